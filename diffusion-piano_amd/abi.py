@@ -1,0 +1,86 @@
+"""ctypes mirror of include/pianosim.h (descriptor structs and constants)."""
+
+import ctypes as C
+
+NKEY = 88
+NHAND = 2
+HAND_NBODY = 25
+HAND_NDOF = 26
+HAND_NGEOM = 20
+HAND_NACT = 22
+HAND_NTENDON = 4
+NFINGER = 5
+NV = NKEY + NHAND * HAND_NDOF
+NU = NHAND * HAND_NACT
+NACTION = NU + 1
+MAX_CAPPAIRS = 768
+MAX_NOTES = 16
+MAX_CONTACTS_LIMIT = 48
+NTERMS = 5
+FIRST, MID, LAST = 0, 1, 2
+
+d = C.c_double
+i32 = C.c_int32
+
+
+def _arr(t, *dims):
+    for n in reversed(dims):
+        t = t * n
+    return t
+
+
+class ContactParam(C.Structure):
+    _fields_ = [("solref", _arr(d, 2)), ("solimp", _arr(d, 5)), ("friction", d)]
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [
+        ("timestep", d), ("n_substeps", i32), ("gravity", _arr(d, 3)),
+        ("key_pos", _arr(d, NKEY, 3)), ("key_half", _arr(d, NKEY, 3)),
+        ("key_anchor", _arr(d, NKEY, 3)), ("key_mass", _arr(d, NKEY)),
+        ("key_inertia", _arr(d, NKEY)), ("key_armature", _arr(d, NKEY)),
+        ("key_damping", _arr(d, NKEY)), ("key_stiffness", _arr(d, NKEY)),
+        ("key_springref", _arr(d, NKEY)), ("key_range", _arr(d, NKEY, 2)),
+        ("base_pos", _arr(d, 3)), ("base_half", _arr(d, 3)),
+        ("piano_contact", ContactParam),
+        ("limit_solref", _arr(d, 2)), ("limit_solimp", _arr(d, 5)),
+        ("body_parent", _arr(i32, NHAND, HAND_NBODY)),
+        ("body_pos", _arr(d, NHAND, HAND_NBODY, 3)), ("body_quat", _arr(d, NHAND, HAND_NBODY, 4)),
+        ("body_mass", _arr(d, NHAND, HAND_NBODY)), ("body_ipos", _arr(d, NHAND, HAND_NBODY, 3)),
+        ("body_inertia", _arr(d, NHAND, HAND_NBODY, 6)),
+        ("dof_body", _arr(i32, NHAND, HAND_NDOF)), ("dof_type", _arr(i32, NHAND, HAND_NDOF)),
+        ("dof_axis", _arr(d, NHAND, HAND_NDOF, 3)), ("dof_range", _arr(d, NHAND, HAND_NDOF, 2)),
+        ("dof_limited", _arr(i32, NHAND, HAND_NDOF)), ("dof_damping", _arr(d, NHAND, HAND_NDOF)),
+        ("dof_armature", _arr(d, NHAND, HAND_NDOF)), ("dof_obs_order", _arr(i32, NHAND, HAND_NDOF)),
+        ("geom_body", _arr(i32, NHAND, HAND_NGEOM)), ("geom_pos", _arr(d, NHAND, HAND_NGEOM, 3)),
+        ("geom_axis", _arr(d, NHAND, HAND_NGEOM, 3)), ("geom_halflen", _arr(d, NHAND, HAND_NGEOM)),
+        ("geom_radius", _arr(d, NHAND, HAND_NGEOM)), ("root_geom_count", i32),
+        ("hand_contact", ContactParam),
+        ("site_body", _arr(i32, NHAND, NFINGER)), ("site_pos", _arr(d, NHAND, NFINGER, 3)),
+        ("tendon_dof", _arr(i32, NHAND, HAND_NTENDON, 2)),
+        ("tendon_coef", _arr(d, NHAND, HAND_NTENDON, 2)),
+        ("act_kind", _arr(i32, NHAND, HAND_NACT)), ("act_target", _arr(i32, NHAND, HAND_NACT)),
+        ("act_kp", _arr(d, NHAND, HAND_NACT)), ("act_ctrlrange", _arr(d, NHAND, HAND_NACT, 2)),
+        ("act_forcelimited", _arr(i32, NHAND, HAND_NACT)),
+        ("act_forcerange", _arr(d, NHAND, HAND_NACT, 2)),
+        ("n_cappairs", i32), ("cappair", _arr(i32, MAX_CAPPAIRS, 2)),
+        ("key_body_invweight", _arr(d, NKEY)), ("key_dof_invweight", _arr(d, NKEY)),
+        ("body_invweight", _arr(d, NHAND, HAND_NBODY)), ("dof_invweight", _arr(d, NHAND, HAND_NDOF)),
+    ]
+
+
+class SongDesc(C.Structure):
+    _fields_ = [("T", i32), ("goal", C.POINTER(C.c_float)), ("count", C.POINTER(i32)),
+                ("keys", C.POINTER(i32)), ("fingers", C.POINTER(i32))]
+
+
+class TaskCfg(C.Structure):
+    _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
+                ("wrong_press_termination", i32), ("energy_penalty_coef", d),
+                ("pgs_iterations", i32), ("max_contacts", i32)]
+
+
+def obs_dim(cfg: TaskCfg) -> int:
+    """goal (L+1)*89 + fingering 10 (if enabled) + piano/state 88 + sustain 1 + 2*26."""
+    return (cfg.n_steps_lookahead + 1) * (NKEY + 1) + (10 if cfg.fingering_reward else 0) \
+        + NKEY + 1 + NHAND * HAND_NDOF

@@ -1,0 +1,209 @@
+/*
+ * pianosim.h - C-ABI of the MI355X batched PianoWithShadowHands environment.
+ *
+ * The reference has no FFI for this path: its boundary is the Python VecEnv
+ * `parallelized_base_v2.VectorizedPianoEnv` (parallelized_base_v2.py:21-67), whose
+ * per-env work is dm_control `composer.Environment.step/reset` driving MuJoCo
+ * `mj_step` on a `PianoWithShadowHands` task (robopianist/suite/tasks/
+ * piano_with_shadow_hands.py:49-449). These entry points are what that VecEnv binds
+ * (see INTEGRATION.md for the ctypes stub):
+ *
+ *   ps_create        <- VectorizedPianoEnv.__init__ (parallelized_base_v2.py:22-46):
+ *                       builds N tasks + physics (tasks/base.py:45-197,
+ *                       piano_with_shadow_hands.py:98-128).
+ *   ps_reset         <- VectorizedPianoEnv.reset (parallelized_base_v2.py:48-51) ->
+ *                       composer reset: mj_resetData + initialize_episode
+ *                       (piano_with_shadow_hands.py:169-174, piano.py:145-152).
+ *   ps_step          <- VectorizedPianoEnv.step (parallelized_base_v2.py:53-60) ->
+ *                       before_step (:176-186), 10 x mj_step + Piano.after_substep
+ *                       (piano.py:154-192), after_step (:188-204), observables
+ *                       (:371-449), CompositeReward.compute (composite_reward.py:46-56),
+ *                       termination (:213-220), auto-reset after LAST.
+ *   ps_get_state /   <- physics.data.qpos/qvel/qacc_warmstart/ctrl + task._t_idx
+ *   ps_set_state        (teacher-forced parity; no reference equivalent beyond
+ *                       physics.set_state).
+ *   ps_set_applied   <- physics.bind(joints).qfrc_applied (piano_with_shadow_hands_test.py:239).
+ *   ps_reward_terms  <- CompositeReward.reward_terms (composite_reward.py:62-64).
+ *
+ * Conventions: all array arguments of ps_reset/ps_step/ps_get_state/ps_set_state are
+ * DEVICE pointers (e.g. torch-ROCm tensors' data_ptr()) and the calls are asynchronous
+ * on the caller's HIP stream (`stream` = hipStream_t, NULL = default stream). Return
+ * value 0 = OK, < 0 = error; ps_last_error() gives a thread-local message. No C++
+ * exception crosses the ABI. One handle per device; handles are independent.
+ */
+#ifndef PIANOSIM_H
+#define PIANOSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- fixed topology (robopianist: 88-key piano + 2 Shadow Hand E3M5 + 2 forearm DOFs) */
+#define PS_NKEY 88          /* piano_constants.py:22 */
+#define PS_NHAND 2          /* right, left (tasks/base.py:116-135) */
+#define PS_HAND_NBODY 25    /* forearm + wrist + palm + 4x4 fingers(+lf metacarpal) + 5 thumb */
+#define PS_HAND_NDOF 26     /* shadow_hand_constants.py:21 NQ=24, + forearm_tx/ty */
+#define PS_HAND_NGEOM 20    /* authored capsule colliders per hand */
+#define PS_HAND_NACT 22     /* shadow_hand_constants.py:22 NU=20, + 2 forearm position actuators */
+#define PS_HAND_NTENDON 4   /* FFJ0, MFJ0, RFJ0, LFJ0 fixed tendons */
+#define PS_NFINGER 5        /* fingertip sites th, ff, mf, rf, lf (shadow_hand_constants.py:33-40) */
+#define PS_NV (PS_NKEY + PS_NHAND * PS_HAND_NDOF)     /* 140 */
+#define PS_NU (PS_NHAND * PS_HAND_NACT)               /* 44 */
+#define PS_NACTION (PS_NU + 1)                        /* 45: hands + sustain */
+#define PS_MAX_CAPPAIRS 768 /* capsule-capsule candidate pairs after filtering */
+#define PS_MAX_NOTES 16     /* notes per control step in the song tables */
+
+/* Per-geom contact parameters (MuJoCo geom attributes). */
+typedef struct {
+  double solref[2];   /* timeconst, dampratio */
+  double solimp[5];   /* d0, dwidth, width, midpoint, power */
+  double friction;    /* sliding friction (condim 3, pyramidal) */
+} ps_contact_param;
+
+/* Compiled model ("mjModel" for this task), produced by the host model compiler
+ * (diffusion-piano_amd/model.py). Lengths in metres, angles in radians. */
+typedef struct {
+  double timestep;          /* tasks/base.py:28 */
+  int32_t n_substeps;       /* control 0.05 / physics 0.005 (tasks/base.py:28-31) */
+  double gravity[3];
+  /* piano keys (piano_mjcf.py:64-400), sorted by key number */
+  double key_pos[PS_NKEY][3];      /* body position (world) */
+  double key_half[PS_NKEY][3];     /* box half sizes */
+  double key_anchor[PS_NKEY][3];   /* hinge position in the key body frame */
+  double key_mass[PS_NKEY];
+  double key_inertia[PS_NKEY];     /* moment of inertia about the hinge axis (no armature) */
+  double key_armature[PS_NKEY];
+  double key_damping[PS_NKEY];
+  double key_stiffness[PS_NKEY];
+  double key_springref[PS_NKEY];
+  double key_range[PS_NKEY][2];
+  double base_pos[3], base_half[3];  /* static piano base box */
+  ps_contact_param piano_contact;
+  double limit_solref[2], limit_solimp[5];
+  /* hands: [0]=right, [1]=left. Bodies in MuJoCo tree order; parent -1 = world. */
+  int32_t body_parent[PS_NHAND][PS_HAND_NBODY];
+  double body_pos[PS_NHAND][PS_HAND_NBODY][3];   /* in parent frame */
+  double body_quat[PS_NHAND][PS_HAND_NBODY][4];  /* w x y z, in parent frame */
+  double body_mass[PS_NHAND][PS_HAND_NBODY];
+  double body_ipos[PS_NHAND][PS_HAND_NBODY][3];  /* COM in body frame */
+  double body_inertia[PS_NHAND][PS_HAND_NBODY][6]; /* about COM, body frame: xx yy zz xy xz yz */
+  /* DOFs in MuJoCo qpos order (each hinge/slide at its body origin). */
+  int32_t dof_body[PS_NHAND][PS_HAND_NDOF];
+  int32_t dof_type[PS_NHAND][PS_HAND_NDOF];     /* 0 = hinge, 1 = slide */
+  double dof_axis[PS_NHAND][PS_HAND_NDOF][3];   /* body frame */
+  double dof_range[PS_NHAND][PS_HAND_NDOF][2];
+  int32_t dof_limited[PS_NHAND][PS_HAND_NDOF];
+  double dof_damping[PS_NHAND][PS_HAND_NDOF];
+  double dof_armature[PS_NHAND][PS_HAND_NDOF];
+  int32_t dof_obs_order[PS_NHAND][PS_HAND_NDOF]; /* joints_pos[i] = qpos[dof_obs_order[i]] */
+  /* capsule colliders (body frame segment centre/axis) */
+  int32_t geom_body[PS_NHAND][PS_HAND_NGEOM];
+  double geom_pos[PS_NHAND][PS_HAND_NGEOM][3];
+  double geom_axis[PS_NHAND][PS_HAND_NGEOM][3];
+  double geom_halflen[PS_NHAND][PS_HAND_NGEOM];
+  double geom_radius[PS_NHAND][PS_HAND_NGEOM];
+  int32_t root_geom_count;   /* geoms [0, root_geom_count) belong to the root (forearm) body */
+  ps_contact_param hand_contact;
+  /* fingertip sites (shadow_hand.py:190-207) */
+  int32_t site_body[PS_NHAND][PS_NFINGER];
+  double site_pos[PS_NHAND][PS_NFINGER][3];
+  /* fixed tendons J0 = J2 + J1 (two dofs each) */
+  int32_t tendon_dof[PS_NHAND][PS_HAND_NTENDON][2];
+  double tendon_coef[PS_NHAND][PS_HAND_NTENDON][2];
+  /* position actuators: target = dof (kind 0) or tendon (kind 1) */
+  int32_t act_kind[PS_NHAND][PS_HAND_NACT];
+  int32_t act_target[PS_NHAND][PS_HAND_NACT];
+  double act_kp[PS_NHAND][PS_HAND_NACT];
+  double act_ctrlrange[PS_NHAND][PS_HAND_NACT][2];
+  int32_t act_forcelimited[PS_NHAND][PS_HAND_NACT];
+  double act_forcerange[PS_NHAND][PS_HAND_NACT][2];
+  /* capsule-capsule candidate pairs (global geom index = hand*PS_HAND_NGEOM + g),
+   * after MuJoCo's filtering (same body, parent-child, <exclude>) */
+  int32_t n_cappairs;
+  int32_t cappair[PS_MAX_CAPPAIRS][2];
+  /* mj_setConst-style inverse weights at qpos0 (regulariser scale diagApprox of the soft
+   * constraints): translational body mobility trace(Jp M^-1 Jp^T)/3 and diag(M^-1). */
+  double key_body_invweight[PS_NKEY];
+  double key_dof_invweight[PS_NKEY];
+  double body_invweight[PS_NHAND][PS_HAND_NBODY];
+  double dof_invweight[PS_NHAND][PS_HAND_NDOF];
+} ps_model_desc;
+
+/* Song tables: NoteTrajectory in dense form (music.py:SongTables). */
+typedef struct {
+  int32_t T;
+  const float* goal;       /* [T][89]: keys + sustain */
+  const int32_t* count;    /* [T] */
+  const int32_t* keys;     /* [T][PS_MAX_NOTES] */
+  const int32_t* fingers;  /* [T][PS_MAX_NOTES], 0-4 right, 5-9 left */
+} ps_song_desc;
+
+/* Task options (piano_with_shadow_hands.py:50-66). */
+typedef struct {
+  int32_t n_steps_lookahead;        /* goal rows = lookahead + 1 */
+  int32_t fingering_reward;         /* 1: fingering reward + 'fingering' obs; 0: OT reward */
+  int32_t forearm_reward;           /* 1: add forearm reward term */
+  int32_t wrong_press_termination;
+  double energy_penalty_coef;       /* 5e-3 */
+  int32_t pgs_iterations;           /* constraint solver sweeps per substep */
+  int32_t max_contacts;             /* per env, <= PS_MAX_CONTACTS_LIMIT */
+} ps_task_cfg;
+
+#define PS_MAX_CONTACTS_LIMIT 48
+
+/* step_type values (dm_env.StepType) */
+#define PS_FIRST 0
+#define PS_MID 1
+#define PS_LAST 2
+
+/* Reward term slots of ps_reward_terms (CompositeReward insertion order). */
+#define PS_TERM_KEY_PRESS 0
+#define PS_TERM_SUSTAIN 1
+#define PS_TERM_ENERGY 2
+#define PS_TERM_FINGERING 3   /* fingering_reward or ot_fingering_reward */
+#define PS_TERM_FOREARM 4
+#define PS_NTERMS 5
+
+typedef struct ps_env ps_env;
+
+const char* ps_last_error(void);
+int ps_version(void);
+int ps_obs_dim(const ps_task_cfg* cfg);
+/* sizeof(ps_model_desc), for host-side layout checks. */
+int ps_model_desc_size(void);
+
+int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_task_cfg* cfg,
+              int n_envs, int device, uint64_t seed, ps_env** out);
+void ps_destroy(ps_env* env);
+
+/* Resets envs (all when env_mask == NULL, else where env_mask[i] != 0; device u8[N])
+ * and writes their first observation into obs[N][obs_dim]. */
+int ps_reset(ps_env* env, const uint8_t* env_mask, float* obs, void* stream);
+
+/* action[N][45] in spec units (CanonicalSpecWrapper already applied). Envs whose
+ * previous step was LAST are reset instead and report PS_FIRST (reward 0, discount 1). */
+int ps_step(ps_env* env, const float* action, float* obs, float* reward, float* discount,
+            uint8_t* step_type, void* stream);
+
+/* qpos/qvel/qacc_warmstart [N][140] (MuJoCo dof order: keys, right hand, left hand),
+ * ctrl [N][44], sustain [N], t_idx [N], last [N] (1 if the previous step was LAST). */
+int ps_get_state(ps_env* env, float* qpos, float* qvel, float* qacc_ws, float* ctrl,
+                 float* sustain, int32_t* t_idx, uint8_t* last, void* stream);
+int ps_set_state(ps_env* env, const float* qpos, const float* qvel, const float* qacc_ws,
+                 const float* ctrl, const float* sustain, const int32_t* t_idx,
+                 const uint8_t* last, void* stream);
+/* Generalized applied force [N][140] added every substep until changed (NULL clears). */
+int ps_set_applied(ps_env* env, const float* qfrc_applied, void* stream);
+/* Per-term rewards of the last step, [N][PS_NTERMS]. */
+int ps_reward_terms(ps_env* env, float* terms, void* stream);
+/* Fingertip site positions after the last step/reset, [N][2][5][3] (right, left). */
+int ps_fingertips(ps_env* env, float* xpos, void* stream);
+/* Number of contacts after the last step/reset, [N]. */
+int ps_contact_count(ps_env* env, int32_t* ncon, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

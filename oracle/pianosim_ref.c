@@ -1,0 +1,1178 @@
+/*
+ * pianosim_ref.c - CPU fp64 ORACLE for the batched PianoWithShadowHands step.
+ *
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the checker / CPU baseline. The product (libpianosim.so, HIP) never
+ * links or calls this file.
+ *
+ * Plain sequential restatement of the reference path, one env at a time:
+ *   - task layer: robopianist/suite/tasks/piano_with_shadow_hands.py:176-449,
+ *     robopianist/models/piano/piano.py:154-192, composite_reward.py:46-56,
+ *     shadow_hand.py:380-416, dm_control composer.Environment.step hook order and
+ *     dm_control.utils.rewards.tolerance (gaussian, value_at_margin=0.1);
+ *   - physics: MuJoCo's documented mj_step pipeline for hinge/slide trees (the engine
+ *     itself is an absent third-party dependency, `mujoco>=3.1.1`, setup.py:62):
+ *     kinematics, composite-rigid-body mass matrix + armature, tree LDL (mj_factorI /
+ *     mj_solveLD), recursive Newton-Euler bias, passive spring/damper, position
+ *     actuators (joint + fixed tendon), collision, soft constraints (solref/solimp,
+ *     refsafe), pyramidal friction cones, PGS dual solve warm-started from
+ *     qacc_warmstart, Euler with implicit joint damping (mj_EulerSkip).
+ * Parity status: the task layer is pinned by the reference tests' known answers and the
+ * golden song fixtures (tests/golden/); the physics is "parity unpinned" against MuJoCo
+ * (no mujoco/dm_control/Menagerie in this container, no reference test records numeric
+ * physics state): it is the specification the HIP kernel is checked against.
+ * Deviations from MuJoCo defaults are listed in DESIGN.md ("Physics specification").
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/pianosim.h"
+
+#define NK PS_NKEY
+#define NH PS_NHAND
+#define NB PS_HAND_NBODY
+#define ND PS_HAND_NDOF
+#define NG PS_HAND_NGEOM
+#define NA PS_HAND_NACT
+#define NV PS_NV
+#define MAXCON PS_MAX_CONTACTS_LIMIT
+#define MAXROW (4 * MAXCON + NH * ND * 2 + NK)
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+#define MINVAL 1e-15
+#define KEY_THRESHOLD 0.00872665   /* piano.py:31 */
+#define SUSTAIN_THRESHOLD 0.5      /* piano.py:32 */
+
+typedef struct { double v[3]; } v3;
+
+static inline v3 mk(double a, double b, double c) { v3 r = {{a, b, c}}; return r; }
+static inline v3 add(v3 a, v3 b) { return mk(a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2]); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.v[0] - b.v[0], a.v[1] - b.v[1], a.v[2] - b.v[2]); }
+static inline v3 scl(v3 a, double s) { return mk(a.v[0] * s, a.v[1] * s, a.v[2] * s); }
+static inline double dot(v3 a, v3 b) { return a.v[0] * b.v[0] + a.v[1] * b.v[1] + a.v[2] * b.v[2]; }
+static inline v3 crs(v3 a, v3 b) {
+  return mk(a.v[1] * b.v[2] - a.v[2] * b.v[1], a.v[2] * b.v[0] - a.v[0] * b.v[2],
+            a.v[0] * b.v[1] - a.v[1] * b.v[0]);
+}
+static inline double nrm(v3 a) { return sqrt(dot(a, a)); }
+static inline double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+typedef struct { double m[9]; } m3;  /* row-major */
+static inline v3 mv(m3 R, v3 a) {
+  return mk(R.m[0] * a.v[0] + R.m[1] * a.v[1] + R.m[2] * a.v[2],
+            R.m[3] * a.v[0] + R.m[4] * a.v[1] + R.m[5] * a.v[2],
+            R.m[6] * a.v[0] + R.m[7] * a.v[1] + R.m[8] * a.v[2]);
+}
+static inline v3 mtv(m3 R, v3 a) {
+  return mk(R.m[0] * a.v[0] + R.m[3] * a.v[1] + R.m[6] * a.v[2],
+            R.m[1] * a.v[0] + R.m[4] * a.v[1] + R.m[7] * a.v[2],
+            R.m[2] * a.v[0] + R.m[5] * a.v[1] + R.m[8] * a.v[2]);
+}
+static m3 mm(m3 A, m3 B) {
+  m3 C;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      C.m[3 * i + j] = A.m[3 * i] * B.m[j] + A.m[3 * i + 1] * B.m[3 + j] + A.m[3 * i + 2] * B.m[6 + j];
+  return C;
+}
+static m3 quat2mat(const double* q) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  double w = q[0] / n, x = q[1] / n, y = q[2] / n, z = q[3] / n;
+  m3 R = {{1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+           2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+           2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)}};
+  return R;
+}
+/* Rotation by angle t about unit axis a (Rodrigues). */
+static m3 axisangle(v3 a, double t) {
+  double s = sin(t), c = cos(t), C1 = 1 - c;
+  double x = a.v[0], y = a.v[1], z = a.v[2];
+  m3 R = {{c + x * x * C1, x * y * C1 - z * s, x * z * C1 + y * s,
+           y * x * C1 + z * s, c + y * y * C1, y * z * C1 - x * s,
+           z * x * C1 - y * s, z * y * C1 + x * s, c + z * z * C1}};
+  return R;
+}
+
+/* ------------------------------------------------------------------ model (derived) */
+typedef struct {
+  ps_model_desc d;
+  int dof_parent[NH][ND];     /* MuJoCo dof_parentid within the hand */
+  int body_dofadr[NH][NB];    /* first dof of the body, -1 if none */
+  int body_dofnum[NH][NB];
+  double key_y_lo[NK], key_y_hi[NK];
+} model;
+
+static void derive(model* m) {
+  for (int h = 0; h < NH; h++) {
+    for (int b = 0; b < NB; b++) { m->body_dofadr[h][b] = -1; m->body_dofnum[h][b] = 0; }
+    for (int j = 0; j < ND; j++) {
+      int b = m->d.dof_body[h][j];
+      if (m->body_dofadr[h][b] < 0) m->body_dofadr[h][b] = j;
+      m->body_dofnum[h][b]++;
+    }
+    for (int j = 0; j < ND; j++) {
+      int b = m->d.dof_body[h][j];
+      if (j > m->body_dofadr[h][b]) { m->dof_parent[h][j] = j - 1; continue; }
+      int p = m->d.body_parent[h][b], par = -1;
+      while (p >= 0) {
+        if (m->body_dofnum[h][p] > 0) { par = m->body_dofadr[h][p] + m->body_dofnum[h][p] - 1; break; }
+        p = m->d.body_parent[h][p];
+      }
+      m->dof_parent[h][j] = par;
+    }
+  }
+  for (int k = 0; k < NK; k++) {
+    m->key_y_lo[k] = m->d.key_pos[k][1] - m->d.key_half[k][1];
+    m->key_y_hi[k] = m->d.key_pos[k][1] + m->d.key_half[k][1];
+  }
+}
+
+/* ------------------------------------------------------------------ per-env data */
+typedef struct {
+  int kind;          /* 0 hand-key, 1 hand-base, 2 capsule-capsule */
+  int key;           /* key index for kind 0 */
+  int h1, b1;        /* side 1: hand/body (kind 2) */
+  int h2, b2;        /* side 2: hand/body of the capsule (geom2) */
+  int g1, g2;        /* global geom ids (kind 2: both; kind 0/1: g2 only) */
+  v3 pos, n, t1, t2;
+  double dist;
+} contact;
+
+typedef struct {
+  /* state */
+  double q[NV], v[NV], qacc_ws[NV], ctrl[PS_NU], sustain, applied[NV];
+  int t_idx, last;
+  /* kinematics */
+  m3 R[NH][NB];
+  v3 o[NH][NB], com[NH][NB], axis[NH][ND];
+  double Iw[NH][NB][9];
+  v3 cap0[NH][NG], cap1[NH][NG];
+  m3 keyR[NK];
+  v3 keyc[NK], keyanchor[NK];
+  /* dynamics */
+  double M[NH][ND][ND], Mh[NH][ND][ND], D[NH][ND], Dh[NH][ND];
+  double Mk[NK], Mkh[NK];
+  double bias[NV], passive[NV], actfrc[NV], act_force[PS_NU];
+  /* collision */
+  int ncon;
+  contact con[MAXCON];
+  /* outputs */
+  double terms[PS_NTERMS];
+  double norm_state[NK];
+  int activation[NK];
+} envdata;
+
+struct ref_env {
+  model m;
+  ps_task_cfg cfg;
+  int T;
+  float* goal;
+  int32_t *count, *keys, *fingers;
+  int n;
+  envdata* e;
+};
+typedef struct ref_env ref_env;
+
+/* ------------------------------------------------------------------ kinematics */
+static void kinematics(const model* m, envdata* E) {
+  const ps_model_desc* d = &m->d;
+  for (int h = 0; h < NH; h++) {
+    const double* qh = E->q + NK + h * ND;
+    for (int b = 0; b < NB; b++) {
+      int p = d->body_parent[h][b];
+      m3 Q = quat2mat(d->body_quat[h][b]);
+      v3 pos = mk(d->body_pos[h][b][0], d->body_pos[h][b][1], d->body_pos[h][b][2]);
+      m3 R;
+      v3 o;
+      if (p < 0) { R = Q; o = pos; }
+      else { R = mm(E->R[h][p], Q); o = add(E->o[h][p], mv(E->R[h][p], pos)); }
+      for (int j = m->body_dofadr[h][b]; j >= 0 && j < m->body_dofadr[h][b] + m->body_dofnum[h][b]; j++) {
+        v3 al = mk(d->dof_axis[h][j][0], d->dof_axis[h][j][1], d->dof_axis[h][j][2]);
+        if (d->dof_type[h][j] == 1) {
+          v3 aw = mv(R, al);
+          E->axis[h][j] = aw;
+          o = add(o, scl(aw, qh[j]));
+        } else {
+          R = mm(R, axisangle(al, qh[j]));
+          E->axis[h][j] = mv(R, al);
+        }
+      }
+      E->R[h][b] = R;
+      E->o[h][b] = o;
+      v3 ip = mk(d->body_ipos[h][b][0], d->body_ipos[h][b][1], d->body_ipos[h][b][2]);
+      E->com[h][b] = add(o, mv(R, ip));
+      /* world inertia about COM: R I R^T */
+      const double* I6 = d->body_inertia[h][b];
+      double Il[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
+      double tmp[9];
+      for (int i = 0; i < 3; i++)
+        for (int k = 0; k < 3; k++) {
+          double s = 0;
+          for (int l = 0; l < 3; l++) s += R.m[3 * i + l] * Il[3 * l + k];
+          tmp[3 * i + k] = s;
+        }
+      for (int i = 0; i < 3; i++)
+        for (int k = 0; k < 3; k++) {
+          double s = 0;
+          for (int l = 0; l < 3; l++) s += tmp[3 * i + l] * R.m[3 * k + l];
+          E->Iw[h][b][3 * i + k] = s;
+        }
+    }
+    for (int g = 0; g < NG; g++) {
+      int b = d->geom_body[h][g];
+      v3 c = add(E->o[h][b], mv(E->R[h][b], mk(d->geom_pos[h][g][0], d->geom_pos[h][g][1], d->geom_pos[h][g][2])));
+      v3 a = mv(E->R[h][b], mk(d->geom_axis[h][g][0], d->geom_axis[h][g][1], d->geom_axis[h][g][2]));
+      E->cap0[h][g] = sub(c, scl(a, d->geom_halflen[h][g]));
+      E->cap1[h][g] = add(c, scl(a, d->geom_halflen[h][g]));
+    }
+  }
+  for (int k = 0; k < NK; k++) {
+    double q = E->q[k], c = cos(q), s = sin(q);
+    m3 R = {{c, 0, s, 0, 1, 0, -s, 0, c}};  /* rotation about +y */
+    v3 P = mk(d->key_pos[k][0], d->key_pos[k][1], d->key_pos[k][2]);
+    v3 al = mk(d->key_anchor[k][0], d->key_anchor[k][1], d->key_anchor[k][2]);
+    v3 A = add(P, al);
+    E->keyR[k] = R;
+    E->keyanchor[k] = A;
+    E->keyc[k] = add(A, mv(R, scl(al, -1.0)));
+  }
+}
+
+static v3 site_pos(const model* m, const envdata* E, int h, int s) {
+  const ps_model_desc* d = &m->d;
+  int b = d->site_body[h][s];
+  return add(E->o[h][b], mv(E->R[h][b], mk(d->site_pos[h][s][0], d->site_pos[h][s][1], d->site_pos[h][s][2])));
+}
+
+/* ------------------------------------------------------------------ mass matrix + bias */
+static void dynamics(const model* m, const ps_task_cfg* cfg, envdata* E) {
+  (void)cfg;
+  const ps_model_desc* d = &m->d;
+  const double h_t = d->timestep;
+  v3 g = mk(d->gravity[0], d->gravity[1], d->gravity[2]);
+  for (int h = 0; h < NH; h++) {
+    const double* vh = E->v + NK + h * ND;
+    /* composite inertia about each body origin */
+    double ms[NB];
+    v3 hh[NB];
+    double Is[NB][9];
+    for (int b = 0; b < NB; b++) {
+      double mass = d->body_mass[h][b];
+      v3 dd = sub(E->com[h][b], E->o[h][b]);
+      ms[b] = mass;
+      hh[b] = scl(dd, mass);
+      double d2 = dot(dd, dd);
+      for (int i = 0; i < 3; i++)
+        for (int k = 0; k < 3; k++)
+          Is[b][3 * i + k] = E->Iw[h][b][3 * i + k] + mass * ((i == k ? d2 : 0.0) - dd.v[i] * dd.v[k]);
+    }
+    for (int b = NB - 1; b > 0; b--) {
+      int p = d->body_parent[h][b];
+      v3 r = sub(E->o[h][b], E->o[h][p]);
+      double r2 = dot(r, r), rh = dot(r, hh[b]);
+      for (int i = 0; i < 3; i++)
+        for (int k = 0; k < 3; k++)
+          Is[p][3 * i + k] += Is[b][3 * i + k] + ms[b] * ((i == k ? r2 : 0.0) - r.v[i] * r.v[k]) +
+                              ((i == k ? 2 * rh : 0.0) - r.v[i] * hh[b].v[k] - hh[b].v[i] * r.v[k]);
+      hh[p] = add(hh[p], add(hh[b], scl(r, ms[b])));
+      ms[p] += ms[b];
+    }
+    /* M[i][j] for j ancestor-or-self of i */
+    memset(E->M[h], 0, sizeof(E->M[h]));
+    for (int i = 0; i < ND; i++) {
+      int bi = d->dof_body[h][i];
+      v3 ai = E->axis[h][i], flin, fang;
+      if (d->dof_type[h][i] == 0) {
+        flin = crs(ai, hh[bi]);
+        fang = mk(Is[bi][0] * ai.v[0] + Is[bi][1] * ai.v[1] + Is[bi][2] * ai.v[2],
+                  Is[bi][3] * ai.v[0] + Is[bi][4] * ai.v[1] + Is[bi][5] * ai.v[2],
+                  Is[bi][6] * ai.v[0] + Is[bi][7] * ai.v[1] + Is[bi][8] * ai.v[2]);
+      } else {
+        flin = scl(ai, ms[bi]);
+        fang = crs(hh[bi], ai);
+      }
+      for (int j = i; j >= 0; j = m->dof_parent[h][j]) {
+        int bj = d->dof_body[h][j];
+        v3 aj = E->axis[h][j];
+        double val;
+        if (d->dof_type[h][j] == 0) val = dot(aj, add(fang, crs(sub(E->o[h][bi], E->o[h][bj]), flin)));
+        else val = dot(aj, flin);
+        E->M[h][i][j] = val;
+        E->M[h][j][i] = val;
+      }
+      E->M[h][i][i] += d->dof_armature[h][i];
+    }
+    /* bias forces: RNE, gravity as base acceleration */
+    v3 w[NB], al[NB], vo[NB], ac[NB], F[NB], N[NB];
+    for (int b = 0; b < NB; b++) {
+      int p = d->body_parent[h][b];
+      if (p < 0) {
+        w[b] = mk(0, 0, 0);
+        al[b] = mk(0, 0, 0);
+        vo[b] = mk(0, 0, 0);
+        for (int j = m->body_dofadr[h][b]; j >= 0 && j < m->body_dofadr[h][b] + m->body_dofnum[h][b]; j++)
+          vo[b] = add(vo[b], scl(E->axis[h][j], vh[j]));
+        ac[b] = scl(g, -1.0);
+      } else {
+        v3 r = sub(E->o[h][b], E->o[h][p]);
+        w[b] = w[p];
+        al[b] = al[p];
+        vo[b] = add(vo[p], crs(w[p], r));
+        ac[b] = add(ac[p], add(crs(al[p], r), crs(w[p], crs(w[p], r))));
+        int j = m->body_dofadr[h][b];  /* one hinge per non-root body */
+        v3 a = E->axis[h][j];
+        al[b] = add(al[b], scl(crs(w[p], a), vh[j]));
+        w[b] = add(w[b], scl(a, vh[j]));
+      }
+      v3 dd = sub(E->com[h][b], E->o[h][b]);
+      v3 acom = add(ac[b], add(crs(al[b], dd), crs(w[b], crs(w[b], dd))));
+      F[b] = scl(acom, d->body_mass[h][b]);
+      const double* I = E->Iw[h][b];
+      v3 Ia = mk(I[0] * al[b].v[0] + I[1] * al[b].v[1] + I[2] * al[b].v[2],
+                 I[3] * al[b].v[0] + I[4] * al[b].v[1] + I[5] * al[b].v[2],
+                 I[6] * al[b].v[0] + I[7] * al[b].v[1] + I[8] * al[b].v[2]);
+      v3 Iw = mk(I[0] * w[b].v[0] + I[1] * w[b].v[1] + I[2] * w[b].v[2],
+                 I[3] * w[b].v[0] + I[4] * w[b].v[1] + I[5] * w[b].v[2],
+                 I[6] * w[b].v[0] + I[7] * w[b].v[1] + I[8] * w[b].v[2]);
+      N[b] = add(add(Ia, crs(w[b], Iw)), crs(dd, F[b]));  /* about body origin */
+    }
+    for (int b = NB - 1; b > 0; b--) {
+      int p = d->body_parent[h][b];
+      v3 r = sub(E->o[h][b], E->o[h][p]);
+      N[p] = add(N[p], add(N[b], crs(r, F[b])));
+      F[p] = add(F[p], F[b]);
+    }
+    for (int j = 0; j < ND; j++) {
+      int b = d->dof_body[h][j];
+      E->bias[NK + h * ND + j] = d->dof_type[h][j] == 0 ? dot(E->axis[h][j], N[b]) : dot(E->axis[h][j], F[b]);
+      E->passive[NK + h * ND + j] = -d->dof_damping[h][j] * vh[j];
+    }
+  }
+  for (int k = 0; k < NK; k++) {
+    v3 r = sub(E->keyc[k], E->keyanchor[k]);
+    /* generalized gravity force about +y: (r x m g).y ; bias = -that */
+    E->bias[k] = -d->key_mass[k] * (r.v[2] * g.v[0] - r.v[0] * g.v[2]);
+    E->passive[k] = -d->key_stiffness[k] * (E->q[k] - d->key_springref[k]) - d->key_damping[k] * E->v[k];
+    E->Mk[k] = d->key_inertia[k] + d->key_armature[k];
+    E->Mkh[k] = E->Mk[k] + h_t * d->key_damping[k];
+  }
+  /* actuation (mj_fwdActuation: ctrl clamped to ctrlrange, force clamped to forcerange) */
+  memset(E->actfrc, 0, sizeof(E->actfrc));
+  for (int h = 0; h < NH; h++) {
+    const double* qh = E->q + NK + h * ND;
+    for (int a = 0; a < NA; a++) {
+      double len;
+      int tg = d->act_target[h][a];
+      if (d->act_kind[h][a] == 0) len = qh[tg];
+      else len = d->tendon_coef[h][tg][0] * qh[d->tendon_dof[h][tg][0]] + d->tendon_coef[h][tg][1] * qh[d->tendon_dof[h][tg][1]];
+      double c = clampd(E->ctrl[h * NA + a], d->act_ctrlrange[h][a][0], d->act_ctrlrange[h][a][1]);
+      double f = d->act_kp[h][a] * (c - len);
+      if (d->act_forcelimited[h][a]) f = clampd(f, d->act_forcerange[h][a][0], d->act_forcerange[h][a][1]);
+      E->act_force[h * NA + a] = f;
+      if (d->act_kind[h][a] == 0) E->actfrc[NK + h * ND + tg] += f;
+      else {
+        E->actfrc[NK + h * ND + d->tendon_dof[h][tg][0]] += d->tendon_coef[h][tg][0] * f;
+        E->actfrc[NK + h * ND + d->tendon_dof[h][tg][1]] += d->tendon_coef[h][tg][1] * f;
+      }
+    }
+  }
+}
+
+/* mj_factorI on the tree-sparse hand matrix (in place: L below diag, D separately) */
+static void factor(const model* m, int h, double A[ND][ND], double* D) {
+  for (int k = ND - 1; k >= 0; k--) {
+    if (A[k][k] < MINVAL) A[k][k] = MINVAL;
+    for (int i = m->dof_parent[h][k]; i >= 0; i = m->dof_parent[h][i]) {
+      double tmp = A[k][i] / A[k][k];
+      for (int j = i; j >= 0; j = m->dof_parent[h][j]) A[i][j] -= tmp * A[k][j];
+      A[k][i] = tmp;
+    }
+  }
+  for (int k = 0; k < ND; k++) D[k] = A[k][k];
+}
+
+/* x <- L^-T x (first phase of mj_solveLD) */
+static void solve_LT(const model* m, int h, double A[ND][ND], double* x) {
+  for (int k = ND - 1; k >= 0; k--)
+    for (int i = m->dof_parent[h][k]; i >= 0; i = m->dof_parent[h][i]) x[i] -= A[k][i] * x[k];
+}
+/* x <- L^-1 x (last phase) */
+static void solve_L(const model* m, int h, double A[ND][ND], double* x) {
+  for (int k = 0; k < ND; k++)
+    for (int i = m->dof_parent[h][k]; i >= 0; i = m->dof_parent[h][i]) x[k] -= A[k][i] * x[i];
+}
+static void solve_full(const model* m, envdata* E, int implicit, const double* b, double* x) {
+  memcpy(x, b, sizeof(double) * NV);
+  for (int k = 0; k < NK; k++) x[k] /= implicit ? E->Mkh[k] : E->Mk[k];
+  for (int h = 0; h < NH; h++) {
+    double* xh = x + NK + h * ND;
+    double(*A)[ND] = implicit ? E->Mh[h] : E->M[h];
+    double* D = implicit ? E->Dh[h] : E->D[h];
+    solve_LT(m, h, A, xh);
+    for (int k = 0; k < ND; k++) xh[k] /= D[k];
+    solve_L(m, h, A, xh);
+  }
+}
+
+/* ------------------------------------------------------------------ collision */
+static void make_frame(v3 n, v3* t1, v3* t2) {
+  v3 e = fabs(n.v[2]) < 0.5 ? mk(0, 0, 1) : mk(1, 0, 0);
+  v3 a = crs(n, e);
+  *t1 = scl(a, 1.0 / nrm(a));
+  *t2 = crs(n, *t1);
+}
+
+/* point (world) vs box: signed distance, normal box->point, contact midpoint */
+static double sphere_box(v3 p, double r, v3 c, m3 R, const double* hs, v3* nout, v3* posout) {
+  v3 pl = mtv(R, sub(p, c));
+  v3 q;
+  int outside = 0;
+  for (int i = 0; i < 3; i++) {
+    q.v[i] = clampd(pl.v[i], -hs[i], hs[i]);
+    if (q.v[i] != pl.v[i]) outside = 1;
+  }
+  v3 n, mid;
+  double dist;
+  if (outside) {
+    v3 dv = sub(pl, q);
+    double dn = nrm(dv);
+    n = scl(dv, 1.0 / dn);
+    dist = dn - r;
+    mid = add(q, scl(n, 0.5 * dist));
+  } else {
+    int ax = 0;
+    double best = hs[0] - fabs(pl.v[0]);
+    for (int i = 1; i < 3; i++) {
+      double s = hs[i] - fabs(pl.v[i]);
+      if (s < best) { best = s; ax = i; }
+    }
+    n = mk(0, 0, 0);
+    n.v[ax] = pl.v[ax] >= 0 ? 1.0 : -1.0;
+    dist = -best - r;
+    mid = add(pl, scl(n, 0.5 * (best - r)));
+  }
+  *nout = mv(R, n);
+  *posout = add(c, mv(R, mid));
+  return dist;
+}
+
+/* argmin over t in [0,1] of the outside distance of segment a + t d to the box */
+static double seg_box_t(v3 a, v3 dv, const double* hs) {
+  double bp[8];
+  int nb = 0;
+  bp[nb++] = 0.0;
+  for (int i = 0; i < 3; i++) {
+    if (dv.v[i] == 0.0) continue;
+    for (int sgn = -1; sgn <= 1; sgn += 2) {
+      double t = (sgn * hs[i] - a.v[i]) / dv.v[i];
+      if (t > 0.0 && t < 1.0) bp[nb++] = t;
+    }
+  }
+  bp[nb++] = 1.0;
+  for (int i = 1; i < nb; i++)  /* insertion sort */
+    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { double t = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = t; }
+  double bestf = INFINITY, bestt = 0.0;
+  for (int s = 0; s + 1 < nb; s++) {
+    double lo = bp[s], hi = bp[s + 1];
+    if (!(hi > lo)) continue;
+    double mid = 0.5 * (lo + hi), num = 0.0, den = 0.0;
+    for (int i = 0; i < 3; i++) {
+      double x = a.v[i] + mid * dv.v[i];
+      double tgt = x > hs[i] ? hs[i] : (x < -hs[i] ? -hs[i] : 0.0);
+      if (tgt == 0.0 && fabs(x) <= hs[i]) continue;
+      num -= (a.v[i] - tgt) * dv.v[i];
+      den += dv.v[i] * dv.v[i];
+    }
+    double t = den > 0.0 ? clampd(num / den, lo, hi) : lo;
+    double f = 0.0;
+    for (int i = 0; i < 3; i++) {
+      double e = fabs(a.v[i] + t * dv.v[i]) - hs[i];
+      if (e > 0) f += e * e;
+    }
+    if (f < bestf) { bestf = f; bestt = t; }
+  }
+  if (bestf <= 0.0) {  /* intersecting: midpoint of the slab-clipped interval */
+    double tin = 0.0, tout = 1.0;
+    int empty = 0;
+    for (int i = 0; i < 3; i++) {
+      if (fabs(dv.v[i]) < 1e-12) {
+        if (fabs(a.v[i]) > hs[i]) empty = 1;
+        continue;
+      }
+      double t1 = (-hs[i] - a.v[i]) / dv.v[i], t2 = (hs[i] - a.v[i]) / dv.v[i];
+      if (t1 > t2) { double t = t1; t1 = t2; t2 = t; }
+      if (t1 > tin) tin = t1;
+      if (t2 < tout) tout = t2;
+    }
+    if (!empty && tin <= tout) bestt = 0.5 * (tin + tout);
+  }
+  return bestt;
+}
+
+static int add_contact(envdata* E, int maxc, const contact* c) {
+  if (E->ncon >= maxc) return 0;
+  E->con[E->ncon++] = *c;
+  return 1;
+}
+
+/* capsule (geom2) vs box (geom1): up to 2 contacts, normal box -> capsule */
+static void capsule_box(envdata* E, int maxc, contact proto, v3 p0, v3 p1, double r, v3 c, m3 R, const double* hs) {
+  v3 n, pos;
+  int found = 0;
+  for (int e = 0; e < 2; e++) {
+    double dist = sphere_box(e == 0 ? p0 : p1, r, c, R, hs, &n, &pos);
+    if (dist <= 0.0) {
+      contact cc = proto;
+      cc.pos = pos; cc.n = n; cc.dist = dist;
+      make_frame(n, &cc.t1, &cc.t2);
+      add_contact(E, maxc, &cc);
+      found = 1;
+    }
+  }
+  if (found) return;
+  v3 a = mtv(R, sub(p0, c)), b = mtv(R, sub(p1, c));
+  double t = seg_box_t(a, sub(b, a), hs);
+  v3 p = add(p0, scl(sub(p1, p0), t));
+  double dist = sphere_box(p, r, c, R, hs, &n, &pos);
+  if (dist <= 0.0) {
+    contact cc = proto;
+    cc.pos = pos; cc.n = n; cc.dist = dist;
+    make_frame(n, &cc.t1, &cc.t2);
+    add_contact(E, maxc, &cc);
+  }
+}
+
+/* closest points between segments p1-q1 and p2-q2 (Ericson, RTCD 5.1.9) */
+static void seg_seg(v3 p1, v3 q1, v3 p2, v3 q2, v3* c1, v3* c2) {
+  v3 d1 = sub(q1, p1), d2 = sub(q2, p2), r = sub(p1, p2);
+  double a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r), s, t;
+  const double eps = 1e-12;
+  if (a <= eps && e <= eps) { s = t = 0; }
+  else if (a <= eps) { s = 0; t = clampd(f / e, 0, 1); }
+  else {
+    double c = dot(d1, r);
+    if (e <= eps) { t = 0; s = clampd(-c / a, 0, 1); }
+    else {
+      double b = dot(d1, d2), den = a * e - b * b;
+      s = den != 0.0 ? clampd((b * f - c * e) / den, 0, 1) : 0.0;
+      t = (b * s + f) / e;
+      if (t < 0) { t = 0; s = clampd(-c / a, 0, 1); }
+      else if (t > 1) { t = 1; s = clampd((b - c) / a, 0, 1); }
+    }
+  }
+  *c1 = add(p1, scl(d1, s));
+  *c2 = add(p2, scl(d2, t));
+}
+
+static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
+  const ps_model_desc* d = &m->d;
+  int maxc = cfg->max_contacts;
+  E->ncon = 0;
+  m3 I3 = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+  v3 bc = mk(d->base_pos[0], d->base_pos[1], d->base_pos[2]);
+  for (int h = 0; h < NH; h++) {
+    for (int g = 0; g < NG; g++) {
+      v3 p0 = E->cap0[h][g], p1 = E->cap1[h][g];
+      double r = d->geom_radius[h][g];
+      double lo[3], hi[3];
+      for (int i = 0; i < 3; i++) {
+        lo[i] = fmin(p0.v[i], p1.v[i]) - r;
+        hi[i] = fmax(p0.v[i], p1.v[i]) + r;
+      }
+      contact proto;
+      memset(&proto, 0, sizeof(proto));
+      proto.h2 = h; proto.b2 = d->geom_body[h][g]; proto.g2 = h * NG + g;
+      for (int k = 0; k < NK; k++) {
+        /* conservative broadphase: key AABB over its motion */
+        if (hi[1] < m->key_y_lo[k] || lo[1] > m->key_y_hi[k]) continue;
+        if (lo[2] > d->key_pos[k][2] + d->key_half[k][2] + 0.02) continue;
+        if (hi[0] < d->key_pos[k][0] - d->key_half[k][0] - 0.02 || lo[0] > d->key_pos[k][0] + d->key_half[k][0] + 0.02) continue;
+        proto.kind = 0; proto.key = k;
+        capsule_box(E, maxc, proto, p0, p1, r, E->keyc[k], E->keyR[k], d->key_half[k]);
+      }
+      proto.kind = 1; proto.key = -1;
+      capsule_box(E, maxc, proto, p0, p1, r, bc, I3, d->base_half);
+    }
+  }
+  for (int i = 0; i < d->n_cappairs; i++) {
+    int ga = d->cappair[i][0], gb = d->cappair[i][1];
+    int ha = ga / NG, la = ga % NG, hb = gb / NG, lb = gb % NG;
+    v3 ca = scl(add(E->cap0[ha][la], E->cap1[ha][la]), 0.5), cb = scl(add(E->cap0[hb][lb], E->cap1[hb][lb]), 0.5);
+    double ra = d->geom_radius[ha][la], rb = d->geom_radius[hb][lb];
+    double bound = d->geom_halflen[ha][la] + d->geom_halflen[hb][lb] + ra + rb;
+    if (nrm(sub(ca, cb)) > bound) continue;
+    v3 c1, c2;
+    seg_seg(E->cap0[ha][la], E->cap1[ha][la], E->cap0[hb][lb], E->cap1[hb][lb], &c1, &c2);
+    v3 dv = sub(c2, c1);
+    double dn = nrm(dv);
+    double dist = dn - ra - rb;
+    if (dist > 0.0) continue;
+    contact cc;
+    memset(&cc, 0, sizeof(cc));
+    cc.kind = 2; cc.key = -1;
+    cc.h1 = ha; cc.b1 = d->geom_body[ha][la]; cc.g1 = ga;
+    cc.h2 = hb; cc.b2 = d->geom_body[hb][lb]; cc.g2 = gb;
+    cc.n = dn > 1e-9 ? scl(dv, 1.0 / dn) : mk(0, 0, 1);
+    cc.dist = dist;
+    cc.pos = add(c1, scl(cc.n, ra + 0.5 * dist));
+    make_frame(cc.n, &cc.t1, &cc.t2);
+    if (!add_contact(E, maxc, &cc)) break;
+  }
+}
+
+/* ------------------------------------------------------------------ constraints */
+typedef struct {
+  double J[NV];   /* dense over all dofs (sparse in practice) */
+  double y[NV];   /* L^-T J^T */
+  double Aii, R, aref, b, f;
+  int closed;     /* free key limit row (solved in closed form) */
+} row;
+
+static double impedance(const double* si, double pos) {
+  double d0 = clampd(si[0], MINIMP, MAXIMP), dw = clampd(si[1], MINIMP, MAXIMP);
+  double width = si[2], mid = si[3], power = si[4];
+  double x = fabs(pos) / width, imp;
+  if (x >= 1.0 || width <= MINVAL) imp = dw;
+  else {
+    double y;
+    if (power == 1.0) y = x;
+    else if (x <= mid) y = pow(x, power) / pow(mid, power - 1.0);
+    else y = 1.0 - pow(1.0 - x, power) / pow(1.0 - mid, power - 1.0);
+    imp = d0 + y * (dw - d0);
+  }
+  return clampd(imp, MINIMP, MAXIMP);
+}
+
+/* Jacobian row of a point on a hand body along direction u, accumulated with sign */
+static void jac_point(const model* m, const envdata* E, int h, int b, v3 p, v3 u, double sgn, double* J) {
+  const ps_model_desc* d = &m->d;
+  for (int bb = b; bb >= 0; bb = d->body_parent[h][bb]) {
+    for (int j = m->body_dofadr[h][bb]; j >= 0 && j < m->body_dofadr[h][bb] + m->body_dofnum[h][bb]; j++) {
+      double val = d->dof_type[h][j] == 0 ? dot(u, crs(E->axis[h][j], sub(p, E->o[h][bb]))) : dot(u, E->axis[h][j]);
+      J[NK + h * ND + j] += sgn * val;
+    }
+  }
+}
+
+static void contact_jac(const model* m, const envdata* E, const contact* c, v3 u, double* J) {
+  memset(J, 0, sizeof(double) * NV);
+  jac_point(m, E, c->h2, c->b2, c->pos, u, 1.0, J);
+  if (c->kind == 2) jac_point(m, E, c->h1, c->b1, c->pos, u, -1.0, J);
+  else if (c->kind == 0) {
+    v3 ay = mk(0, 1, 0);
+    J[c->key] -= dot(u, crs(ay, sub(c->pos, E->keyanchor[c->key])));
+  }
+}
+
+static double dotv(const double* a, const double* b) {
+  double s = 0;
+  for (int i = 0; i < NV; i++) s += a[i] * b[i];
+  return s;
+}
+
+/* diagApprox: MuJoCo's constant regulariser scale from invweight0 (mj_diagApprox) */
+static void row_finish(const model* m, envdata* E, row* r, double pos, const double* solref, const double* solimp,
+                       double diag_approx, const double* qacc_smooth) {
+  const ps_model_desc* d = &m->d;
+  memcpy(r->y, r->J, sizeof(r->y));
+  for (int h = 0; h < NH; h++) solve_LT(m, h, E->M[h], r->y + NK + h * ND);
+  double A = 0;
+  for (int k = 0; k < NK; k++) A += r->y[k] * r->y[k] / E->Mk[k];
+  for (int h = 0; h < NH; h++)
+    for (int j = 0; j < ND; j++) A += r->y[NK + h * ND + j] * r->y[NK + h * ND + j] / E->D[h][j];
+  r->Aii = A;
+  double imp = impedance(solimp, pos);
+  double dmax = clampd(solimp[1], MINIMP, MAXIMP);
+  double tc = fmax(solref[0], 2.0 * d->timestep), dr = solref[1];
+  double K = 1.0 / (dmax * dmax * tc * tc * dr * dr), B = 2.0 / (dmax * tc);
+  r->aref = -B * dotv(r->J, E->v) - K * imp * pos;
+  r->R = fmax(MINVAL, (1.0 - imp) / imp * diag_approx);
+  r->b = dotv(r->J, qacc_smooth) - r->aref;
+  r->f = 0;
+}
+
+static void mix_param(const ps_contact_param* a, const ps_contact_param* b, double* solref, double* solimp, double* mu) {
+  for (int i = 0; i < 2; i++) solref[i] = 0.5 * (a->solref[i] + b->solref[i]);
+  for (int i = 0; i < 5; i++) solimp[i] = 0.5 * (a->solimp[i] + b->solimp[i]);
+  *mu = fmax(a->friction, b->friction);
+}
+
+static _Thread_local row g_rows[MAXROW];
+int ref_debug_level = 0;
+#include <stdio.h>
+
+static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
+  const ps_model_desc* d = &m->d;
+  const double h_t = d->timestep;
+  kinematics(m, E);
+  dynamics(m, cfg, E);
+  collide(m, cfg, E);
+  for (int h = 0; h < NH; h++) {
+    memcpy(E->Mh[h], E->M[h], sizeof(E->M[h]));
+    for (int j = 0; j < ND; j++) E->Mh[h][j][j] += h_t * d->dof_damping[h][j];
+    factor(m, h, E->M[h], E->D[h]);
+    factor(m, h, E->Mh[h], E->Dh[h]);
+  }
+  double fsmooth[NV], qacc_smooth[NV];
+  for (int i = 0; i < NV; i++) fsmooth[i] = E->passive[i] + E->actfrc[i] + E->applied[i] - E->bias[i];
+  solve_full(m, E, 0, fsmooth, qacc_smooth);
+
+  /* constraint rows: hand limits, key limits (coupled first, free ones closed-form), contacts */
+  int keyhit[NK];
+  memset(keyhit, 0, sizeof(keyhit));
+  for (int c = 0; c < E->ncon; c++)
+    if (E->con[c].kind == 0) keyhit[E->con[c].key] = 1;
+  int nr = 0;
+  for (int h = 0; h < NH; h++)
+    for (int j = 0; j < ND; j++) {
+      if (!d->dof_limited[h][j]) continue;
+      double q = E->q[NK + h * ND + j];
+      for (int side = 0; side < 2; side++) {
+        double dist = side == 0 ? q - d->dof_range[h][j][0] : d->dof_range[h][j][1] - q;
+        if (dist >= 0.0) continue;
+        row* r = &g_rows[nr++];
+        memset(r->J, 0, sizeof(r->J));
+        r->J[NK + h * ND + j] = side == 0 ? 1.0 : -1.0;
+        r->closed = 0;
+        row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->dof_invweight[h][j], qacc_smooth);
+      }
+    }
+  for (int pass = 0; pass < 2; pass++)
+    for (int k = 0; k < NK; k++) {
+      if ((pass == 0) != (keyhit[k] != 0)) continue;
+      for (int side = 0; side < 2; side++) {
+        double dist = side == 0 ? E->q[k] - d->key_range[k][0] : d->key_range[k][1] - E->q[k];
+        if (dist >= 0.0) continue;
+        row* r = &g_rows[nr++];
+        memset(r->J, 0, sizeof(r->J));
+        r->J[k] = side == 0 ? 1.0 : -1.0;
+        r->closed = pass;
+        row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->key_dof_invweight[k], qacc_smooth);
+      }
+    }
+  for (int c = 0; c < E->ncon; c++) {
+    contact* cc = &E->con[c];
+    double solref[2], solimp[5], mu;
+    mix_param(cc->kind == 2 ? &d->hand_contact : &d->piano_contact, &d->hand_contact, solref, solimp, &mu);
+    double Jn[NV], Jt1[NV], Jt2[NV];
+    contact_jac(m, E, cc, cc->n, Jn);
+    contact_jac(m, E, cc, cc->t1, Jt1);
+    contact_jac(m, E, cc, cc->t2, Jt2);
+    double tran = d->body_invweight[cc->h2][cc->b2];
+    if (cc->kind == 0) tran += d->key_body_invweight[cc->key];
+    else if (cc->kind == 2) tran += d->body_invweight[cc->h1][cc->b1];
+    double diag = (1.0 + mu * mu) * tran;
+    for (int e = 0; e < 4; e++) {
+      row* r = &g_rows[nr++];
+      const double* Jt = e < 2 ? Jt1 : Jt2;
+      double s = (e & 1) ? -mu : mu;
+      for (int i = 0; i < NV; i++) r->J[i] = Jn[i] + s * Jt[i];
+      r->closed = 0;
+      row_finish(m, E, r, cc->dist, solref, solimp, diag, qacc_smooth);
+    }
+  }
+
+  /* PGS on the coupled rows; closed-form free key rows */
+  double w[NV];
+  memset(w, 0, sizeof(w));
+  for (int i = 0; i < nr; i++) {
+    row* r = &g_rows[i];
+    if (r->closed) { r->f = fmax(0.0, -r->b / (r->Aii + r->R)); continue; }
+    r->f = fmax(0.0, -(dotv(r->J, E->qacc_ws) - r->aref) / r->R);
+    for (int k = 0; k < NV; k++) w[k] += r->y[k] * r->f;
+  }
+  for (int it = 0; it < cfg->pgs_iterations; it++) {
+    for (int i = 0; i < nr; i++) {
+      row* r = &g_rows[i];
+      if (r->closed) continue;
+      double res = r->b + r->R * r->f;
+      for (int k = 0; k < NK; k++) res += r->y[k] * w[k] / E->Mk[k];
+      for (int h = 0; h < NH; h++)
+        for (int j = 0; j < ND; j++) res += r->y[NK + h * ND + j] * w[NK + h * ND + j] / E->D[h][j];
+      double fn = fmax(0.0, r->f - res / (r->Aii + r->R));
+      if (ref_debug_level > 1 && i < 4) printf("it %d row %d f %.5g res %.5g fn %.5g\n", it, i, r->f, res, fn);
+      double df = fn - r->f;
+      if (df != 0.0)
+        for (int k = 0; k < NV; k++) w[k] += r->y[k] * df;
+      r->f = fn;
+    }
+  }
+  for (int i = 0; i < nr; i++)
+    if (g_rows[i].closed)
+      for (int k = 0; k < NK; k++) w[k] += g_rows[i].y[k] * g_rows[i].f;
+  /* qfrc_constraint = J^T f = L^T w */
+  double F[NV];
+  for (int k = 0; k < NK; k++) F[k] = fsmooth[k] + w[k];
+  for (int h = 0; h < NH; h++) {
+    double* wh = w + NK + h * ND;
+    double out[ND];
+    for (int j = 0; j < ND; j++) out[j] = wh[j];
+    for (int k = 0; k < ND; k++)
+      for (int i = m->dof_parent[h][k]; i >= 0; i = m->dof_parent[h][i]) out[i] += E->M[h][k][i] * wh[k];
+    for (int j = 0; j < ND; j++) F[NK + h * ND + j] = fsmooth[NK + h * ND + j] + out[j];
+  }
+  double qacc[NV], qacc_e[NV];
+  solve_full(m, E, 0, F, qacc);
+  if (ref_debug_level) {
+    for (int i = 0; i < nr; i++) if (!g_rows[i].closed)
+      printf("row %d Aii %.4g R %.4g aref %.4g b %.4g f %.4g\n", i, g_rows[i].Aii, g_rows[i].R, g_rows[i].aref, g_rows[i].b, g_rows[i].f);
+  }
+  solve_full(m, E, 1, F, qacc_e);
+  memcpy(E->qacc_ws, qacc, sizeof(qacc));
+  for (int i = 0; i < NV; i++) {
+    E->v[i] += h_t * qacc_e[i];
+    E->q[i] += h_t * E->v[i];
+  }
+}
+
+/* ------------------------------------------------------------------ task layer */
+static double tolerance(double x, double lo, double hi, double margin) {
+  if (x >= lo && x <= hi) return 1.0;
+  double dd = (x < lo ? lo - x : x - hi) / margin;
+  double scale = sqrt(-2.0 * log(0.1));
+  return exp(-0.5 * (dd * scale) * (dd * scale));
+}
+
+/* rectangular assignment, min cost; rows n <= cols mm (e-maxx Hungarian). Returns sum of
+ * tol(cost) over the n assigned pairs. */
+static double hungarian_tol(int n, int mm, double c[][PS_MAX_NOTES > 10 ? PS_MAX_NOTES : 10]) {
+  double u[12], v[PS_MAX_NOTES + 2], minv[PS_MAX_NOTES + 2];
+  int p[PS_MAX_NOTES + 2], way[PS_MAX_NOTES + 2], used[PS_MAX_NOTES + 2];
+  for (int i = 0; i <= n; i++) u[i] = 0;
+  for (int j = 0; j <= mm; j++) { v[j] = 0; p[j] = 0; way[j] = 0; }
+  for (int i = 1; i <= n; i++) {
+    p[0] = i;
+    int j0 = 0;
+    for (int j = 0; j <= mm; j++) { minv[j] = INFINITY; used[j] = 0; }
+    do {
+      used[j0] = 1;
+      int i0 = p[j0], j1 = 0;
+      double delta = INFINITY;
+      for (int j = 1; j <= mm; j++)
+        if (!used[j]) {
+          double cur = c[i0 - 1][j - 1] - u[i0] - v[j];
+          if (cur < minv[j]) { minv[j] = cur; way[j] = j0; }
+          if (minv[j] < delta) { delta = minv[j]; j1 = j; }
+        }
+      for (int j = 0; j <= mm; j++)
+        if (used[j]) { u[p[j]] += delta; v[j] -= delta; }
+        else minv[j] -= delta;
+      j0 = j1;
+    } while (p[j0] != 0);
+    do { int j1 = way[j0]; p[j0] = p[j1]; j0 = j1; } while (j0);
+  }
+  double s = 0;
+  for (int j = 1; j <= mm; j++)
+    if (p[j]) s += tolerance(c[p[j] - 1][j - 1], 0.0, 0.01, 0.1);
+  return s;
+}
+
+static v3 key_target(const model* m, const envdata* E, int k) {
+  /* key geom xpos + [0.35*size_x, 0, 0.5*size_z] (piano_with_shadow_hands.py:310-313) */
+  v3 p = E->keyc[k];
+  p.v[0] += 0.35 * m->d.key_half[k][0];
+  p.v[2] += 0.5 * m->d.key_half[k][2];
+  return p;
+}
+
+static const float* goal_row(const ref_env* R, int t) { return R->goal + (size_t)t * (NK + 1); }
+
+static void write_obs(ref_env* R, envdata* E, float* obs, int t_obs) {
+  const ps_model_desc* d = &R->m.d;
+  int L = R->cfg.n_steps_lookahead, o = 0;
+  for (int j = 0; j <= L; j++)
+    for (int k = 0; k <= NK; k++) {
+      int t = t_obs + j;
+      obs[o++] = t < R->T ? goal_row(R, t)[k] : 0.0f;
+    }
+  if (R->cfg.fingering_reward) {
+    float fs[10] = {0};
+    for (int i = 0; i < R->count[t_obs]; i++) {
+      int f = R->fingers[t_obs * PS_MAX_NOTES + i];
+      if (f < 5) fs[f < 0 ? f + 5 : f] = 1.0f;
+      else fs[5 + f - 5] = 1.0f;
+    }
+    for (int i = 0; i < 10; i++) obs[o++] = fs[i];
+  }
+  for (int k = 0; k < NK; k++) obs[o++] = (float)E->norm_state[k];
+  obs[o++] = (float)E->sustain;
+  for (int h = 0; h < NH; h++)
+    for (int j = 0; j < ND; j++) obs[o++] = (float)E->q[NK + h * ND + d->dof_obs_order[h][j]];
+}
+
+static void key_state(const model* m, envdata* E) {
+  for (int k = 0; k < NK; k++) {
+    double lo = m->d.key_range[k][0], hi = m->d.key_range[k][1];
+    double s = clampd(E->q[k], lo, hi);
+    E->norm_state[k] = s / hi;
+    E->activation[k] = fabs(s - hi) <= KEY_THRESHOLD;
+  }
+}
+
+static void reset_env(ref_env* R, envdata* E, float* obs) {
+  memset(E->q, 0, sizeof(E->q));
+  memset(E->v, 0, sizeof(E->v));
+  memset(E->qacc_ws, 0, sizeof(E->qacc_ws));
+  memset(E->ctrl, 0, sizeof(E->ctrl));
+  E->sustain = 0;
+  E->t_idx = 0;
+  E->last = 0;
+  kinematics(&R->m, E);
+  collide(&R->m, &R->cfg, E);
+  key_state(&R->m, E);
+  memset(E->terms, 0, sizeof(E->terms));
+  if (obs) write_obs(R, E, obs, 0);
+}
+
+static void control_step(ref_env* R, envdata* E, const float* a, float* obs, float* rew, float* disc, uint8_t* st) {
+  const model* m = &R->m;
+  const ps_model_desc* d = &m->d;
+  if (E->last) {
+    reset_env(R, E, obs);
+    *rew = 0.0f; *disc = 1.0f; *st = PS_FIRST;
+    return;
+  }
+  for (int i = 0; i < PS_NU; i++) E->ctrl[i] = a[i];
+  E->sustain = a[PS_NU];
+  for (int s = 0; s < d->n_substeps; s++) step_physics(m, &R->cfg, E);
+  kinematics(m, E);   /* mj_step1 at the final state (legacy_step) */
+  collide(m, &R->cfg, E);
+  key_state(m, E);
+  int sustain_act = E->sustain >= SUSTAIN_THRESHOLD;
+  int t_cur = E->t_idx;  /* goal_current = goal at pre-increment t */
+  const float* gc = goal_row(R, t_cur);
+  E->t_idx += 1;
+  int t_new = E->t_idx;
+  int terminal = t_new == R->T;
+  int failure = 0;
+  for (int k = 0; k < NK; k++) if (gc[k] == 0.0f && E->activation[k]) failure = 1;
+  /* rewards */
+  double kp = 0;
+  int non = 0;
+  double acc = 0;
+  for (int k = 0; k < NK; k++)
+    if (gc[k] != 0.0f) { acc += tolerance(gc[k] - E->norm_state[k], 0, 0.05, 0.5); non++; }
+  if (non > 0) kp += 0.5 * (acc / non);
+  kp += 0.5 * (1.0 - (double)failure);
+  double sus = tolerance(gc[NK] - (double)sustain_act, 0, 0.05, 0.5);
+  double energy = 0;
+  for (int h = 0; h < NH; h++)
+    for (int a2 = 0; a2 < NA; a2++) {
+      int tg = d->act_target[h][a2];
+      const double* vh = E->v + NK + h * ND;
+      double vel = d->act_kind[h][a2] == 0 ? vh[tg]
+                   : d->tendon_coef[h][tg][0] * vh[d->tendon_dof[h][tg][0]] + d->tendon_coef[h][tg][1] * vh[d->tendon_dof[h][tg][1]];
+      energy += fabs(E->act_force[h * NA + a2]) * fabs(vel);
+    }
+  energy *= -R->cfg.energy_penalty_coef;
+  double fing = 0;
+  if (R->cfg.fingering_reward) {
+    double sum = 0;
+    int cnt = 0;
+    for (int hand = 0; hand < 2; hand++)  /* rh list then lh list */
+      for (int i = 0; i < R->count[t_cur]; i++) {
+        int f = R->fingers[t_cur * PS_MAX_NOTES + i], k = R->keys[t_cur * PS_MAX_NOTES + i];
+        int is_rh = f < 5;
+        if (is_rh != (hand == 0)) continue;
+        int site = is_rh ? (f < 0 ? f + 5 : f) : f - 5;
+        v3 tip = site_pos(m, E, hand, site);
+        sum += tolerance(nrm(sub(key_target(m, E, k), tip)), 0, 0.01, 0.1);
+        cnt++;
+      }
+    fing = cnt ? sum / cnt : 0.0;
+  } else {
+    int keys[NK], K = 0;
+    for (int k = 0; k < NK; k++) if (gc[k] != 0.0f) keys[K++] = k;
+    if (K == 0) fing = 1.0;
+    else {
+      v3 tips[10];
+      for (int i = 0; i < 5; i++) { tips[i] = site_pos(m, E, 1, i); tips[5 + i] = site_pos(m, E, 0, i); }
+      int KK = K > PS_MAX_NOTES ? PS_MAX_NOTES : K;
+      double c[PS_MAX_NOTES > 10 ? PS_MAX_NOTES : 10][PS_MAX_NOTES > 10 ? PS_MAX_NOTES : 10];
+      double s;
+      if (KK <= 10) {
+        for (int j = 0; j < KK; j++)
+          for (int i = 0; i < 10; i++) c[j][i] = nrm(sub(key_target(m, E, keys[j]), tips[i]));
+        s = hungarian_tol(KK, 10, c);
+        fing = s / KK;
+      } else {
+        for (int i = 0; i < 10; i++)
+          for (int j = 0; j < KK; j++) c[i][j] = nrm(sub(key_target(m, E, keys[j]), tips[i]));
+        s = hungarian_tol(10, KK, c);
+        fing = s / 10;
+      }
+    }
+  }
+  double fore = 0;
+  if (R->cfg.forearm_reward) {
+    int hit = 0;
+    for (int c = 0; c < E->ncon; c++) {
+      const contact* cc = &E->con[c];
+      if (cc->kind != 2) continue;
+      int la = cc->g1 % NG, lb = cc->g2 % NG;
+      if (cc->g1 / NG != cc->g2 / NG && la < d->root_geom_count && lb < d->root_geom_count) hit = 1;
+    }
+    fore = hit ? 0.0 : 0.5;
+  }
+  E->terms[PS_TERM_KEY_PRESS] = kp;
+  E->terms[PS_TERM_SUSTAIN] = sus;
+  E->terms[PS_TERM_ENERGY] = energy;
+  E->terms[PS_TERM_FINGERING] = fing;
+  E->terms[PS_TERM_FOREARM] = fore;
+  double total = kp + sus + energy + fing + fore;
+  double discount = 1.0;
+  if (!terminal && R->cfg.wrong_press_termination && failure) { terminal = 1; discount = 0.0; }
+  /* observation at t_new; at t_new == T the goal/fingering observables keep their
+   * previous value (piano_with_shadow_hands.py:377-378, 392-393) */
+  write_obs(R, E, obs, t_new < R->T ? t_new : t_new - 1);
+  *rew = (float)total;
+  *disc = (float)discount;
+  *st = terminal ? PS_LAST : PS_MID;
+  E->last = terminal;
+}
+
+/* ------------------------------------------------------------------ API */
+ref_env* ref_create(const ps_model_desc* md, const ps_song_desc* song, const ps_task_cfg* cfg, int n) {
+  ref_env* R = (ref_env*)calloc(1, sizeof(ref_env));
+  R->m.d = *md;
+  derive(&R->m);
+  R->cfg = *cfg;
+  if (R->cfg.max_contacts > MAXCON) R->cfg.max_contacts = MAXCON;
+  R->T = song->T;
+  R->goal = (float*)malloc(sizeof(float) * song->T * (NK + 1));
+  memcpy(R->goal, song->goal, sizeof(float) * song->T * (NK + 1));
+  R->count = (int32_t*)malloc(sizeof(int32_t) * song->T);
+  memcpy(R->count, song->count, sizeof(int32_t) * song->T);
+  R->keys = (int32_t*)malloc(sizeof(int32_t) * song->T * PS_MAX_NOTES);
+  memcpy(R->keys, song->keys, sizeof(int32_t) * song->T * PS_MAX_NOTES);
+  R->fingers = (int32_t*)malloc(sizeof(int32_t) * song->T * PS_MAX_NOTES);
+  memcpy(R->fingers, song->fingers, sizeof(int32_t) * song->T * PS_MAX_NOTES);
+  R->n = n;
+  R->e = (envdata*)calloc((size_t)n, sizeof(envdata));
+  for (int i = 0; i < n; i++) reset_env(R, &R->e[i], NULL);
+  return R;
+}
+
+void ref_destroy(ref_env* R) {
+  if (!R) return;
+  free(R->goal); free(R->count); free(R->keys); free(R->fingers); free(R->e); free(R);
+}
+
+int ref_obs_dim(const ref_env* R) {
+  return (R->cfg.n_steps_lookahead + 1) * (NK + 1) + (R->cfg.fingering_reward ? 10 : 0) + NK + 1 + NH * ND;
+}
+
+void ref_reset(ref_env* R, const uint8_t* mask, float* obs) {
+  int od = ref_obs_dim(R);
+  for (int i = 0; i < R->n; i++)
+    if (!mask || mask[i]) reset_env(R, &R->e[i], obs + (size_t)i * od);
+}
+
+void ref_step(ref_env* R, const float* action, float* obs, float* rew, float* disc, uint8_t* st) {
+  int od = ref_obs_dim(R);
+  for (int i = 0; i < R->n; i++)
+    control_step(R, &R->e[i], action + (size_t)i * PS_NACTION, obs + (size_t)i * od, rew + i, disc + i, st + i);
+}
+
+void ref_get_state(const ref_env* R, double* q, double* v, double* qacc_ws, double* ctrl, double* sustain,
+                   int32_t* t_idx, uint8_t* last) {
+  for (int i = 0; i < R->n; i++) {
+    const envdata* E = &R->e[i];
+    if (q) memcpy(q + (size_t)i * NV, E->q, sizeof(E->q));
+    if (v) memcpy(v + (size_t)i * NV, E->v, sizeof(E->v));
+    if (qacc_ws) memcpy(qacc_ws + (size_t)i * NV, E->qacc_ws, sizeof(E->qacc_ws));
+    if (ctrl) memcpy(ctrl + (size_t)i * PS_NU, E->ctrl, sizeof(E->ctrl));
+    if (sustain) sustain[i] = E->sustain;
+    if (t_idx) t_idx[i] = E->t_idx;
+    if (last) last[i] = (uint8_t)E->last;
+  }
+}
+
+void ref_set_state(ref_env* R, const double* q, const double* v, const double* qacc_ws, const double* ctrl,
+                   const double* sustain, const int32_t* t_idx, const uint8_t* last) {
+  for (int i = 0; i < R->n; i++) {
+    envdata* E = &R->e[i];
+    if (q) memcpy(E->q, q + (size_t)i * NV, sizeof(E->q));
+    if (v) memcpy(E->v, v + (size_t)i * NV, sizeof(E->v));
+    if (qacc_ws) memcpy(E->qacc_ws, qacc_ws + (size_t)i * NV, sizeof(E->qacc_ws));
+    if (ctrl) memcpy(E->ctrl, ctrl + (size_t)i * PS_NU, sizeof(E->ctrl));
+    if (sustain) E->sustain = sustain[i];
+    if (t_idx) E->t_idx = t_idx[i];
+    if (last) E->last = last[i];
+    kinematics(&R->m, E);
+    collide(&R->m, &R->cfg, E);
+    key_state(&R->m, E);
+  }
+}
+
+void ref_set_applied(ref_env* R, const double* qfrc) {
+  for (int i = 0; i < R->n; i++) {
+    if (qfrc) memcpy(R->e[i].applied, qfrc + (size_t)i * NV, sizeof(R->e[i].applied));
+    else memset(R->e[i].applied, 0, sizeof(R->e[i].applied));
+  }
+}
+
+void ref_reward_terms(const ref_env* R, double* terms) {
+  for (int i = 0; i < R->n; i++) memcpy(terms + (size_t)i * PS_NTERMS, R->e[i].terms, sizeof(double) * PS_NTERMS);
+}
+
+void ref_fingertips(const ref_env* R, double* xpos) {
+  for (int i = 0; i < R->n; i++)
+    for (int h = 0; h < NH; h++)
+      for (int s = 0; s < PS_NFINGER; s++) {
+        v3 p = site_pos(&R->m, &R->e[i], h, s);
+        for (int c = 0; c < 3; c++) xpos[(((size_t)i * NH + h) * PS_NFINGER + s) * 3 + c] = p.v[c];
+      }
+}
+
+void ref_contact_count(const ref_env* R, int32_t* ncon) {
+  for (int i = 0; i < R->n; i++) ncon[i] = R->e[i].ncon;
+}
+
+/* Single-substep hook for teacher-forced physics parity (no task layer). */
+void ref_physics_substep(ref_env* R) {
+  for (int i = 0; i < R->n; i++) step_physics(&R->m, &R->cfg, &R->e[i]);
+}
+
+/* Exposed helpers for unit tests */
+double ref_tolerance(double x, double lo, double hi, double margin) { return tolerance(x, lo, hi, margin); }
+double ref_assignment_tol(int n, int mm, const double* cost) {
+  double c[PS_MAX_NOTES > 10 ? PS_MAX_NOTES : 10][PS_MAX_NOTES > 10 ? PS_MAX_NOTES : 10];
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < mm; j++) c[i][j] = cost[i * mm + j];
+  return hungarian_tol(n, mm, c);
+}
+
+/* Debug hook for tests: dense mass matrix (before factorization) and bias of env i. */
+void ref_debug_dynamics(ref_env* R, int i, double* Mout, double* bias) {
+  envdata* E = &R->e[i];
+  kinematics(&R->m, E);
+  dynamics(&R->m, &R->cfg, E);
+  memset(Mout, 0, sizeof(double) * NV * NV);
+  for (int k = 0; k < NK; k++) Mout[k * NV + k] = E->Mk[k];
+  for (int h = 0; h < NH; h++)
+    for (int a = 0; a < ND; a++)
+      for (int b = 0; b < ND; b++) Mout[(NK + h * ND + a) * NV + NK + h * ND + b] = E->M[h][a][b];
+  memcpy(bias, E->bias, sizeof(double) * NV);
+}
+/* Body COM positions [2][25][3] of env i (after kinematics). */
+void ref_debug_com(ref_env* R, int i, double* com) {
+  envdata* E = &R->e[i];
+  kinematics(&R->m, E);
+  for (int h = 0; h < NH; h++)
+    for (int b = 0; b < NB; b++)
+      for (int c = 0; c < 3; c++) com[(h * NB + b) * 3 + c] = E->com[h][b].v[c];
+}
+/* Contacts of env i: info[c] = {kind, key, g1, g2}, data[c] = {dist, pos[3], n[3]} */
+int ref_debug_contacts(ref_env* R, int i, int32_t* info, double* data) {
+  envdata* E = &R->e[i];
+  for (int c = 0; c < E->ncon; c++) {
+    info[4 * c] = E->con[c].kind; info[4 * c + 1] = E->con[c].key;
+    info[4 * c + 2] = E->con[c].g1; info[4 * c + 3] = E->con[c].g2;
+    data[7 * c] = E->con[c].dist;
+    for (int k = 0; k < 3; k++) { data[7 * c + 1 + k] = E->con[c].pos.v[k]; data[7 * c + 4 + k] = E->con[c].n.v[k]; }
+  }
+  return E->ncon;
+}

@@ -1,0 +1,152 @@
+"""ctypes loader for the CPU oracle (oracle/pianosim_ref.c).
+
+TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg. Never imported by the product package.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "liboracle.so"
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        L.ref_create.restype = C.c_void_p
+        L.ref_create.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.ref_destroy.argtypes = [C.c_void_p]
+        L.ref_obs_dim.argtypes = [C.c_void_p]
+        L.ref_reset.argtypes = [C.c_void_p, C.c_void_p, _f32p]
+        L.ref_step.argtypes = [C.c_void_p, _f32p, _f32p, _f32p, _f32p, _u8p]
+        L.ref_get_state.argtypes = [C.c_void_p, _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _u8p]
+        L.ref_set_state.argtypes = [C.c_void_p, _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _u8p]
+        L.ref_set_applied.argtypes = [C.c_void_p, C.c_void_p]
+        L.ref_reward_terms.argtypes = [C.c_void_p, _f64p]
+        L.ref_fingertips.argtypes = [C.c_void_p, _f64p]
+        L.ref_contact_count.argtypes = [C.c_void_p, _i32p]
+        L.ref_physics_substep.argtypes = [C.c_void_p]
+        L.ref_tolerance.restype = C.c_double
+        L.ref_tolerance.argtypes = [C.c_double] * 4
+        L.ref_assignment_tol.restype = C.c_double
+        L.ref_assignment_tol.argtypes = [C.c_int, C.c_int, _f64p]
+        _lib = L
+    return _lib
+
+
+class OracleEnv:
+    """N independent envs stepped sequentially in fp64 (the reference's serial VecEnv)."""
+
+    NV, NU, NACTION = 140, 44, 45
+
+    def __init__(self, model_desc, song_tables, cfg, n_envs: int):
+        from importlib import import_module
+        abi = import_module("diffusion-piano_amd.abi")
+        self._song = song_tables
+        self._goal = np.ascontiguousarray(song_tables.goal, dtype=np.float32)
+        self._count = np.ascontiguousarray(song_tables.count, dtype=np.int32)
+        self._keys = np.ascontiguousarray(song_tables.keys, dtype=np.int32)
+        self._fingers = np.ascontiguousarray(song_tables.fingers, dtype=np.int32)
+        sd = abi.SongDesc()
+        sd.T = song_tables.T
+        sd.goal = self._goal.ctypes.data_as(C.POINTER(C.c_float))
+        sd.count = self._count.ctypes.data_as(C.POINTER(C.c_int32))
+        sd.keys = self._keys.ctypes.data_as(C.POINTER(C.c_int32))
+        sd.fingers = self._fingers.ctypes.data_as(C.POINTER(C.c_int32))
+        self.n = n_envs
+        self._h = lib().ref_create(C.addressof(model_desc), C.addressof(sd), C.addressof(cfg), n_envs)
+        self.obs_dim = lib().ref_obs_dim(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ref_destroy(self._h)
+            self._h = None
+
+    def reset(self, mask=None):
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8).ctypes.data
+        lib().ref_reset(self._h, m, obs)
+        return obs
+
+    def step(self, action):
+        a = np.ascontiguousarray(action, np.float32).reshape(self.n, self.NACTION)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
+        rew = np.zeros(self.n, np.float32)
+        disc = np.zeros(self.n, np.float32)
+        st = np.zeros(self.n, np.uint8)
+        lib().ref_step(self._h, a, obs, rew, disc, st)
+        return obs, rew, disc, st
+
+    def get_state(self):
+        n = self.n
+        out = dict(qpos=np.zeros((n, self.NV)), qvel=np.zeros((n, self.NV)),
+                   qacc_ws=np.zeros((n, self.NV)), ctrl=np.zeros((n, self.NU)),
+                   sustain=np.zeros(n), t_idx=np.zeros(n, np.int32), last=np.zeros(n, np.uint8))
+        lib().ref_get_state(self._h, out["qpos"], out["qvel"], out["qacc_ws"], out["ctrl"],
+                            out["sustain"], out["t_idx"], out["last"])
+        return out
+
+    def set_state(self, s):
+        n = self.n
+        f = lambda k, shape: np.ascontiguousarray(np.asarray(s[k], np.float64).reshape(shape))
+        lib().ref_set_state(self._h, f("qpos", (n, self.NV)), f("qvel", (n, self.NV)),
+                            f("qacc_ws", (n, self.NV)), f("ctrl", (n, self.NU)), f("sustain", (n,)),
+                            np.ascontiguousarray(np.asarray(s["t_idx"], np.int32).reshape(n)),
+                            np.ascontiguousarray(np.asarray(s["last"], np.uint8).reshape(n)))
+
+    def set_applied(self, qfrc):
+        if qfrc is None:
+            lib().ref_set_applied(self._h, None)
+        else:
+            a = np.ascontiguousarray(np.asarray(qfrc, np.float64).reshape(self.n, self.NV))
+            lib().ref_set_applied(self._h, a.ctypes.data)
+            self._applied = a
+
+    def reward_terms(self):
+        t = np.zeros((self.n, 5))
+        lib().ref_reward_terms(self._h, t)
+        return t
+
+    def fingertips(self):
+        x = np.zeros((self.n, 2, 5, 3))
+        lib().ref_fingertips(self._h, x)
+        return x
+
+    def contact_count(self):
+        c = np.zeros(self.n, np.int32)
+        lib().ref_contact_count(self._h, c)
+        return c
+
+    def physics_substep(self):
+        lib().ref_physics_substep(self._h)
+
+
+def tolerance(x, lo, hi, margin):
+    return lib().ref_tolerance(x, lo, hi, margin)
+
+
+def assignment_tol(cost):
+    c = np.ascontiguousarray(cost, np.float64)
+    return lib().ref_assignment_tol(c.shape[0], c.shape[1], c)
