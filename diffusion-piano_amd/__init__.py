@@ -1,1 +1,11 @@
-"""MI355X-native batched PianoWithShadowHands environment."""
+"""MI355X-native batched PianoWithShadowHands environment.
+
+Import with ``importlib.import_module("diffusion-piano_amd")`` (the directory name is the
+package name required by the build layout).
+"""
+
+from . import abi, music, model  # noqa: F401
+from .envs import (  # noqa: F401
+    Array, BatchedPianoEnv, BoundedArray, DEBUG, Environment, StepType, TaskConfig, TimeStep,
+    VectorizedPianoEnv, compile_task, load, obs_layout,
+)

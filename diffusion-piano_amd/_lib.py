@@ -1,0 +1,61 @@
+"""ctypes binding of libpianosim.so (the HIP product). No CPU fallback: if the library or
+a GPU is missing, the calls that need them raise."""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "libpianosim.so"
+
+# Every entry point declared in include/pianosim.h.
+EXPORTS = (
+    "ps_last_error", "ps_version", "ps_obs_dim", "ps_model_desc_size", "ps_create", "ps_destroy",
+    "ps_reset", "ps_step", "ps_get_state", "ps_set_state", "ps_set_applied", "ps_reward_terms",
+    "ps_fingertips", "ps_contact_count",
+)
+
+_lib = None
+
+
+class PianosimError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise PianosimError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
+    L.ps_last_error.restype = C.c_char_p
+    L.ps_version.restype = i32
+    L.ps_obs_dim.argtypes = [vp]
+    L.ps_model_desc_size.restype = i32
+    L.ps_create.argtypes = [vp, vp, vp, i32, i32, u64, C.POINTER(vp)]
+    L.ps_destroy.argtypes = [vp]
+    L.ps_reset.argtypes = [vp, vp, vp, vp]
+    L.ps_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.ps_get_state.argtypes = [vp] * 9
+    L.ps_set_state.argtypes = [vp] * 9
+    L.ps_set_applied.argtypes = [vp, vp, vp]
+    L.ps_reward_terms.argtypes = [vp, vp, vp]
+    L.ps_fingertips.argtypes = [vp, vp, vp]
+    L.ps_contact_count.argtypes = [vp, vp, vp]
+    for name in EXPORTS:
+        if name not in ("ps_last_error", "ps_version", "ps_model_desc_size", "ps_destroy"):
+            getattr(L, name).restype = i32
+    L.ps_destroy.restype = None
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().ps_last_error()
+        raise PianosimError(msg.decode() if msg else f"pianosim error {rc}")

@@ -15,7 +15,8 @@ NU = NHAND * HAND_NACT
 NACTION = NU + 1
 MAX_CAPPAIRS = 768
 MAX_NOTES = 16
-MAX_CONTACTS_LIMIT = 48
+MAX_CONTACTS_LIMIT = 24
+MAX_ROWS = 96
 NTERMS = 5
 FIRST, MID, LAST = 0, 1, 2
 
@@ -77,7 +78,7 @@ class SongDesc(C.Structure):
 class TaskCfg(C.Structure):
     _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
                 ("wrong_press_termination", i32), ("energy_penalty_coef", d),
-                ("pgs_iterations", i32), ("max_contacts", i32)]
+                ("pgs_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32)]
 
 
 def obs_dim(cfg: TaskCfg) -> int:

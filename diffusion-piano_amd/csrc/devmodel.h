@@ -1,0 +1,79 @@
+// Device-side model tables for the pianosim kernels (float, flattened, plus the
+// topology tables the wave-cooperative phases iterate over). Built on the host from a
+// ps_model_desc by build_dev_model() in pianosim.hip.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/pianosim.h"
+
+namespace ps {
+
+constexpr int NK = PS_NKEY;
+constexpr int NH = PS_NHAND;
+constexpr int NB = PS_HAND_NBODY;
+constexpr int ND = PS_HAND_NDOF;
+constexpr int NG = PS_HAND_NGEOM;
+constexpr int NA = PS_HAND_NACT;
+constexpr int NV = PS_NV;
+constexpr int NU = PS_NU;
+constexpr int NBT = NH * NB;   // 50 hand bodies
+constexpr int NDT = NH * ND;   // 52 hand dofs (lane l <-> hand dof l)
+constexpr int NGT = NH * NG;   // 40 capsules
+constexpr int NTT = NH * PS_HAND_NTENDON;
+constexpr int MAXDEP = 9;      // ancestor list length (self + up to 8 ancestors)
+constexpr int MAXLEV = 8;      // body tree levels
+constexpr int MAXCHILD = 5;
+constexpr int MAXCON = 24;     // per-env contact capacity of the GPU workspace
+constexpr int MAXROW = PS_MAX_ROWS;
+constexpr int KEYLANE = 52;    // lane that carries a row's key-dof entry
+constexpr int ROWSTRIDE = 53;  // 52 hand dofs + key entry; odd stride: conflict-free columns
+constexpr int NTRI = MAXDEP * (MAXDEP - 1) / 2;  // (a,b) pairs 1<=a<=b<=8
+
+struct DevModel {
+  float timestep;
+  int nsub;
+  float grav[3];
+  // keys
+  float key_pos[NK][3], key_half[NK][3], key_anchor[NK][3];
+  float key_mass[NK], key_Minv[NK], key_Mhinv[NK], key_damp[NK], key_stiff[NK], key_sref[NK];
+  float key_lo[NK], key_hi[NK], key_ylo[NK], key_yhi[NK], key_binv[NK], key_dinv[NK];
+  float base_pos[3], base_half[3];
+  float pc_solref[2], pc_solimp[5], pc_fric;
+  float hc_solref[2], hc_solimp[5], hc_fric;
+  float lim_solref[2], lim_solimp[5];
+  // hand bodies, global index B = h*NB + b
+  int body_parent[NBT];
+  float body_pos[NBT][3], body_Q[NBT][9], body_mass[NBT], body_ipos[NBT][3], body_I[NBT][6];
+  float body_binv[NBT];
+  int body_dof[NBT], body_ndof[NBT];
+  uint64_t body_pathmask[NBT];  // bit l: hand dof l acts on the body
+  int nlev, lev_start[MAXLEV + 1], lev_body[NBT];
+  int body_nchild[NBT], body_child[NBT][MAXCHILD];
+  // hand dofs, global index g = h*ND + j
+  int dof_body[NDT], dof_type[NDT], dof_limited[NDT];
+  float dof_axis[NDT][3], dof_lo[NDT], dof_hi[NDT], dof_damp[NDT], dof_arm[NDT], dof_dinv[NDT];
+  int dof_depth[NDT], dof_anc[NDT][MAXDEP];
+  uint64_t dof_ancmask[NDT];
+  int dof_ndesc[NDT], dof_desc[NDT][ND];
+  int ndepth, dep_start[MAXDEP + 1], dep_dof[NDT];
+  int dof_act[NDT];          // actuator driving the dof (global index) or -1
+  float dof_act_coef[NDT];
+  int obs_dof[NDT];          // joints_pos order -> global dof
+  // actuators, global a = h*NA + a
+  int act_kind[NU], act_dof0[NU], act_dof1[NU], act_flim[NU];
+  float act_c0[NU], act_c1[NU], act_kp[NU], act_clo[NU], act_chi[NU], act_flo[NU], act_fhi[NU];
+  // capsules
+  int geom_body[NGT];
+  float geom_pos[NGT][3], geom_axis[NGT][3], geom_hl[NGT], geom_r[NGT];
+  int root_geom_count;
+  // fingertip sites
+  int site_body[NH * PS_NFINGER];
+  float site_pos[NH * PS_NFINGER][3];
+  // capsule-capsule pairs
+  int npairs;
+  int pair[PS_MAX_CAPPAIRS][2];
+  // triangular (a,b) table for the LDL update
+  int tri_a[NTRI + 8], tri_b[NTRI + 8];
+};
+
+}  // namespace ps

@@ -1,0 +1,405 @@
+"""Batched PianoWithShadowHands environments on the MI355X kernel.
+
+Host-side mirror of the reference's interface for the hot path:
+
+* :class:`VectorizedPianoEnv` - the VecEnv surface of ``parallelized_base_v2.py:21-67``
+  (``reset() -> obs dict``, ``step(actions) -> (obs dict, rewards, dones)``,
+  ``envs[i].observation_spec()/action_spec()``) plus the ``observation_spec`` /
+  ``action_spec`` attributes of ``parallelized_base.py:87-89``.
+* :class:`BatchedPianoEnv` - the torch-native core: flat ``[N, obs_dim]`` observations,
+  rewards, discounts and dm_env step types as torch-ROCm tensors; no host round trip.
+* :func:`load` - ``robopianist.suite.load`` (suite/__init__.py:50-93) for one env,
+  returning dm_env ``TimeStep`` objects.
+
+Task options follow ``PianoWithShadowHands.__init__`` (piano_with_shadow_hands.py:50-66).
+Every compute call goes through libpianosim.so; there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import math
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Dict, NamedTuple, Optional, Union
+
+import numpy as np
+
+from . import _lib, abi, model as model_lib, music
+
+
+# ---------------------------------------------------------------- dm_env (not installed)
+class StepType(enum.IntEnum):
+    FIRST = abi.FIRST
+    MID = abi.MID
+    LAST = abi.LAST
+
+    def first(self) -> bool:
+        return self is StepType.FIRST
+
+    def mid(self) -> bool:
+        return self is StepType.MID
+
+    def last(self) -> bool:
+        return self is StepType.LAST
+
+
+class TimeStep(NamedTuple):
+    """dm_env.TimeStep: FIRST carries reward/discount None."""
+
+    step_type: Any
+    reward: Any
+    discount: Any
+    observation: Any
+
+    def first(self) -> bool:
+        return self.step_type == StepType.FIRST
+
+    def mid(self) -> bool:
+        return self.step_type == StepType.MID
+
+    def last(self) -> bool:
+        return self.step_type == StepType.LAST
+
+
+class Array(NamedTuple):
+    shape: tuple
+    dtype: Any
+    name: str = ""
+
+
+class BoundedArray(NamedTuple):
+    shape: tuple
+    dtype: Any
+    minimum: np.ndarray
+    maximum: np.ndarray
+    name: str = ""
+
+
+# ---------------------------------------------------------------- task configuration
+@dataclass
+class TaskConfig:
+    """``PianoWithShadowHands`` keyword arguments (piano_with_shadow_hands.py:50-66) plus the
+    solver settings of this implementation."""
+
+    n_steps_lookahead: int = 1
+    n_seconds_lookahead: Optional[float] = None
+    trim_silence: bool = False
+    wrong_press_termination: bool = False
+    initial_buffer_time: float = 0.0
+    disable_fingering_reward: bool = False
+    disable_forearm_reward: bool = False
+    disable_colorization: bool = False  # rendering only: no effect here
+    disable_hand_collisions: bool = False
+    energy_penalty_coef: float = 5e-3
+    control_timestep: float = model_lib.CONTROL_TIMESTEP
+    physics_timestep: float = model_lib.PHYSICS_TIMESTEP
+    pgs_iterations: int = 20
+    max_contacts: int = 20
+
+    def lookahead(self) -> int:
+        if self.n_seconds_lookahead is not None:
+            return int(math.ceil(self.n_seconds_lookahead / self.control_timestep))
+        return self.n_steps_lookahead
+
+
+def _to_sequence(midi) -> music.NoteSequence:
+    if isinstance(midi, music.NoteSequence):
+        return midi
+    if isinstance(midi, (str, Path)):
+        return music.parse_midi(midi)
+    raise TypeError(f"unsupported midi input {type(midi)!r}")
+
+
+def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
+    """-> (ps_model_desc, SongTables, ps_task_cfg) for a song and task options."""
+    if isinstance(midi, music.SongTables):
+        song = midi
+    else:
+        seq = _to_sequence(midi)
+        if cfg.trim_silence:
+            seq = music.trim_silence(seq)
+        song = music.song_tables(seq, cfg.control_timestep, cfg.initial_buffer_time)
+    md = model_lib.build_model(control_timestep=cfg.control_timestep,
+                               physics_timestep=cfg.physics_timestep,
+                               hand_collisions=not cfg.disable_hand_collisions)
+    tc = abi.TaskCfg()
+    tc.n_steps_lookahead = cfg.lookahead()
+    tc.fingering_reward = int(not cfg.disable_fingering_reward and song.has_fingering)
+    tc.forearm_reward = int(not cfg.disable_forearm_reward)
+    tc.wrong_press_termination = int(cfg.wrong_press_termination)
+    tc.energy_penalty_coef = cfg.energy_penalty_coef
+    tc.pgs_iterations = cfg.pgs_iterations
+    tc.max_contacts = min(cfg.max_contacts, abi.MAX_CONTACTS_LIMIT)
+    tc.canonical_actions = int(canonical_actions)
+    return md, song, tc
+
+
+def obs_layout(tc: abi.TaskCfg) -> Dict[str, slice]:
+    """Observation keys in the order the reference driver concatenates them
+    (parallelized_base_v2.py:122-131)."""
+    out, o = {}, 0
+    g = (tc.n_steps_lookahead + 1) * (abi.NKEY + 1)
+    out["goal"] = slice(o, o + g); o += g
+    if tc.fingering_reward:
+        out["fingering"] = slice(o, o + 10); o += 10
+    out["piano/state"] = slice(o, o + abi.NKEY); o += abi.NKEY
+    out["piano/sustain_state"] = slice(o, o + 1); o += 1
+    out["rh_shadow_hand/joints_pos"] = slice(o, o + abi.HAND_NDOF); o += abi.HAND_NDOF
+    out["lh_shadow_hand/joints_pos"] = slice(o, o + abi.HAND_NDOF); o += abi.HAND_NDOF
+    return out
+
+
+# ---------------------------------------------------------------- batched core
+class BatchedPianoEnv:
+    """N envs on one GPU; all tensors live in HBM (torch-ROCm)."""
+
+    def __init__(self, num_envs: int, midi, task: Optional[TaskConfig] = None, device=None,
+                 canonical_actions: bool = True, seed: int = 0):
+        import torch
+
+        self._torch = torch
+        if not torch.cuda.is_available():
+            raise _lib.PianosimError("BatchedPianoEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.task = task or TaskConfig()
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.num_envs = int(num_envs)
+        self.model_desc, self.song, self.task_cfg = compile_task(midi, self.task, canonical_actions)
+        self.canonical_actions = canonical_actions
+        self.obs_dim = abi.obs_dim(self.task_cfg)
+        self.obs_slices = obs_layout(self.task_cfg)
+        self.action_lo, self.action_hi = model_lib.action_spec(self.model_desc)
+        L = _lib.load()
+        self._goal = np.ascontiguousarray(self.song.goal, np.float32)
+        self._count = np.ascontiguousarray(self.song.count, np.int32)
+        self._keys = np.ascontiguousarray(self.song.keys, np.int32)
+        self._fingers = np.ascontiguousarray(self.song.fingers, np.int32)
+        sd = abi.SongDesc()
+        sd.T = self.song.T
+        sd.goal = self._goal.ctypes.data_as(C.POINTER(C.c_float))
+        sd.count = self._count.ctypes.data_as(C.POINTER(C.c_int32))
+        sd.keys = self._keys.ctypes.data_as(C.POINTER(C.c_int32))
+        sd.fingers = self._fingers.ctypes.data_as(C.POINTER(C.c_int32))
+        if L.ps_model_desc_size() != C.sizeof(abi.ModelDesc):
+            raise _lib.PianosimError("ps_model_desc layout mismatch between abi.py and the library")
+        h = C.c_void_p()
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        _lib.check(L.ps_create(C.addressof(self.model_desc), C.addressof(sd), C.addressof(self.task_cfg),
+                               self.num_envs, dev_index, seed, C.byref(h)))
+        self._h = h
+        N = self.num_envs
+        f32 = dict(device=self.device, dtype=torch.float32)
+        self.obs = torch.zeros(N, self.obs_dim, **f32)
+        self.reward = torch.zeros(N, **f32)
+        self.discount = torch.ones(N, **f32)
+        self.step_type = torch.zeros(N, device=self.device, dtype=torch.uint8)
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().ps_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return self._torch.cuda.current_stream(self.device).cuda_stream
+
+    # -- core API (device tensors, asynchronous on the current stream)
+    def reset(self, mask=None):
+        torch = self._torch
+        mptr = None
+        if mask is not None:
+            self._mask = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+            mptr = self._mask.data_ptr()
+        _lib.check(_lib.load().ps_reset(self._h, mptr, self.obs.data_ptr(), self.stream))
+        if mask is None:
+            self.step_type.fill_(abi.FIRST)
+        return self.obs
+
+    def step(self, action):
+        torch = self._torch
+        a = torch.as_tensor(action, device=self.device, dtype=torch.float32)
+        if a.shape != (self.num_envs, abi.NACTION):
+            raise ValueError(f"action must be [{self.num_envs}, {abi.NACTION}], got {tuple(a.shape)}")
+        a = a.contiguous()
+        self._action = a  # keep alive until the kernel ran
+        _lib.check(_lib.load().ps_step(self._h, a.data_ptr(), self.obs.data_ptr(), self.reward.data_ptr(),
+                                       self.discount.data_ptr(), self.step_type.data_ptr(), self.stream))
+        return self.obs, self.reward, self.discount, self.step_type
+
+    def get_state(self) -> Dict[str, Any]:
+        torch = self._torch
+        N = self.num_envs
+        out = dict(qpos=torch.empty(N, abi.NV, device=self.device), qvel=torch.empty(N, abi.NV, device=self.device),
+                   qacc_ws=torch.empty(N, abi.NV, device=self.device), ctrl=torch.empty(N, abi.NU, device=self.device),
+                   sustain=torch.empty(N, device=self.device),
+                   t_idx=torch.empty(N, device=self.device, dtype=torch.int32),
+                   last=torch.empty(N, device=self.device, dtype=torch.uint8))
+        _lib.check(_lib.load().ps_get_state(self._h, *(out[k].data_ptr() for k in
+                                                      ("qpos", "qvel", "qacc_ws", "ctrl", "sustain", "t_idx", "last")),
+                                            self.stream))
+        return out
+
+    def set_state(self, state: Dict[str, Any]):
+        torch = self._torch
+        kinds = dict(qpos=torch.float32, qvel=torch.float32, qacc_ws=torch.float32, ctrl=torch.float32,
+                     sustain=torch.float32, t_idx=torch.int32, last=torch.uint8)
+        keep = {}
+        for k, dt in kinds.items():
+            if k in state and state[k] is not None:
+                keep[k] = torch.as_tensor(state[k], device=self.device).to(dt).contiguous()
+        ptr = lambda k: keep[k].data_ptr() if k in keep else None
+        _lib.check(_lib.load().ps_set_state(self._h, *(ptr(k) for k in kinds), self.stream))
+        self._keep = keep
+
+    def set_applied(self, qfrc):
+        torch = self._torch
+        if qfrc is None:
+            _lib.check(_lib.load().ps_set_applied(self._h, None, self.stream))
+            return
+        t = torch.as_tensor(qfrc, device=self.device, dtype=torch.float32).contiguous()
+        _lib.check(_lib.load().ps_set_applied(self._h, t.data_ptr(), self.stream))
+        self._applied = t
+
+    def reward_terms(self):
+        t = self._torch.empty(self.num_envs, abi.NTERMS, device=self.device)
+        _lib.check(_lib.load().ps_reward_terms(self._h, t.data_ptr(), self.stream))
+        return t
+
+    def fingertips(self):
+        t = self._torch.empty(self.num_envs, 2, 5, 3, device=self.device)
+        _lib.check(_lib.load().ps_fingertips(self._h, t.data_ptr(), self.stream))
+        return t
+
+    def contact_count(self):
+        t = self._torch.empty(self.num_envs, device=self.device, dtype=self._torch.int32)
+        _lib.check(_lib.load().ps_contact_count(self._h, t.data_ptr(), self.stream))
+        return t
+
+    def obs_dict(self, obs=None) -> Dict[str, Any]:
+        obs = self.obs if obs is None else obs
+        return {k: obs[:, s] for k, s in self.obs_slices.items()}
+
+    # -- specs (dm_env)
+    def observation_spec(self) -> Dict[str, Array]:
+        return {k: Array((s.stop - s.start,), np.float64, k) for k, s in self.obs_slices.items()}
+
+    def action_spec(self) -> BoundedArray:
+        if self.canonical_actions:
+            return BoundedArray((abi.NACTION,), np.float32, -np.ones(abi.NACTION, np.float32),
+                                np.ones(abi.NACTION, np.float32), "action")
+        return BoundedArray((abi.NACTION,), np.float32, self.action_lo.astype(np.float32),
+                            self.action_hi.astype(np.float32), "action")
+
+
+# ---------------------------------------------------------------- reference surfaces
+class _EnvView:
+    """``vec_env.envs[i]``: per-env dm_env views (specs; reset/step of that slot)."""
+
+    def __init__(self, parent: "VectorizedPianoEnv", i: int):
+        self._p, self._i = parent, i
+
+    def observation_spec(self):
+        return self._p._core.observation_spec()
+
+    def action_spec(self):
+        return self._p._core.action_spec()
+
+
+class VectorizedPianoEnv:
+    """Drop-in for ``parallelized_base_v2.VectorizedPianoEnv`` (parallelized_base_v2.py:21-67).
+
+    ``reset()`` returns ``{key: [N, d]}``; ``step(actions[N, 45])`` (canonical [-1, 1], as
+    after the reference's per-env ``CanonicalSpecWrapper``) returns ``(obs, rewards, dones)``.
+    With ``return_numpy=True`` the outputs are numpy arrays like the reference's; otherwise
+    they are torch-ROCm tensors that never leave HBM. The task kwargs default to the ones
+    the reference hard-codes (parallelized_base_v2.py:28-39).
+    """
+
+    def __init__(self, num_envs: int, midi_sequence, return_numpy: bool = False, device=None, **task_kwargs):
+        kw = dict(n_steps_lookahead=1, trim_silence=True, wrong_press_termination=False,
+                  initial_buffer_time=0.0, disable_fingering_reward=False, disable_forearm_reward=False,
+                  disable_colorization=False, disable_hand_collisions=False)
+        kw.update(task_kwargs)
+        self.num_envs = num_envs
+        self._core = BatchedPianoEnv(num_envs, midi_sequence, TaskConfig(**kw), device=device)
+        self.return_numpy = return_numpy
+        self.envs = [_EnvView(self, i) for i in range(num_envs)]
+        self.observation_spec = self._core.observation_spec()
+        self.action_spec = self._core.action_spec()
+
+    @property
+    def core(self) -> BatchedPianoEnv:
+        return self._core
+
+    def _out(self, x):
+        if self.return_numpy:
+            return x.detach().cpu().numpy().astype(np.float64)
+        return x
+
+    def reset(self):
+        obs = self._core.reset()
+        return {k: self._out(v) for k, v in self._core.obs_dict(obs).items()}
+
+    def step(self, actions):
+        obs, rew, disc, st = self._core.step(actions)
+        obs_d = {k: self._out(v) for k, v in self._core.obs_dict(obs).items()}
+        dones = st == abi.LAST
+        if self.return_numpy:
+            return obs_d, rew.detach().cpu().numpy().astype(np.float64), dones.cpu().numpy()
+        return obs_d, rew, dones
+
+
+class Environment:
+    """Single-env dm_env facade (``composer_utils.Environment`` + ``CanonicalSpecWrapper``)."""
+
+    def __init__(self, midi, task: Optional[TaskConfig] = None, device=None):
+        self._core = BatchedPianoEnv(1, midi, task, device=device)
+
+    def reset(self) -> TimeStep:
+        obs = self._core.reset()
+        return TimeStep(StepType.FIRST, None, None,
+                        {k: v[0].detach().cpu().numpy() for k, v in self._core.obs_dict(obs).items()})
+
+    def step(self, action) -> TimeStep:
+        a = self._core._torch.as_tensor(np.asarray(action, np.float32).reshape(1, -1), device=self._core.device)
+        obs, rew, disc, st = self._core.step(a)
+        o = {k: v[0].detach().cpu().numpy() for k, v in self._core.obs_dict(obs).items()}
+        t = StepType(int(st[0]))
+        if t == StepType.FIRST:
+            return TimeStep(t, None, None, o)
+        return TimeStep(t, float(rew[0]), float(disc[0]), o)
+
+    def observation_spec(self):
+        return self._core.observation_spec()
+
+    def action_spec(self):
+        return self._core.action_spec()
+
+    @property
+    def core(self):
+        return self._core
+
+
+DEBUG = ["RoboPianist-debug-TwinkleTwinkleLittleStar-v0"]
+_DEBUG_SONGS = {"RoboPianist-debug-TwinkleTwinkleLittleStar-v0": music.twinkle_twinkle_little_star_one_hand}
+
+
+def song_for(environment_name: str, midi_file=None) -> music.NoteSequence:
+    if midi_file is not None:
+        return music.parse_midi(midi_file)
+    if environment_name not in _DEBUG_SONGS:
+        raise ValueError(f"Unknown environment {environment_name}. Available environments: {DEBUG}")
+    return _DEBUG_SONGS[environment_name]()
+
+
+def load(environment_name: str, midi_file=None, seed=None, task_kwargs=None, device=None) -> Environment:
+    """``robopianist.suite.load`` (suite/__init__.py:50-93) for the debug songs / MIDI files."""
+    return Environment(song_for(environment_name, midi_file), TaskConfig(**(task_kwargs or {})), device=device)

@@ -317,11 +317,17 @@ def _subtree_mass(bodies, root):
     return total
 
 
-def build_model(pgs_dt: float = PHYSICS_TIMESTEP) -> abi.ModelDesc:
-    """Compile the scene into a ``ps_model_desc``."""
+def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: float = PHYSICS_TIMESTEP,
+                hand_collisions: bool = True) -> abi.ModelDesc:
+    """Compile the scene into a ``ps_model_desc``.
+
+    ``hand_collisions=False`` is ``disable_hand_collisions`` (piano_with_shadow_hands.py:476-489):
+    every hand collider gets contype=1, conaffinity=0, so no hand geom pair collides
+    (hands still collide with the piano, whose conaffinity is 1).
+    """
     m = abi.ModelDesc()
-    m.timestep = PHYSICS_TIMESTEP
-    m.n_substeps = int(round(CONTROL_TIMESTEP / PHYSICS_TIMESTEP))
+    m.timestep = physics_timestep
+    m.n_substeps = int(round(control_timestep / physics_timestep))
     m.gravity[:] = (0.0, 0.0, -9.81)
     for k, (pos, half, black) in enumerate(piano_keys()):
         m.key_pos[k][:] = pos
@@ -338,7 +344,7 @@ def build_model(pgs_dt: float = PHYSICS_TIMESTEP) -> abi.ModelDesc:
         m.key_range[k][:] = (0.0, BLACK_KEY_MAX_ANGLE if black else WHITE_KEY_MAX_ANGLE)
     m.base_pos[:] = BASE_POS
     m.base_half[:] = BASE_SIZE
-    m.piano_contact.solref[:] = (2 * PHYSICS_TIMESTEP, 1.0)
+    m.piano_contact.solref[:] = (2 * physics_timestep, 1.0)
     m.piano_contact.solimp[:] = (0.9, 0.95, 0.001, 0.5, 2.0)
     m.piano_contact.friction = 1.0
     m.limit_solref[:] = (0.02, 1.0)
@@ -405,7 +411,7 @@ def build_model(pgs_dt: float = PHYSICS_TIMESTEP) -> abi.ModelDesc:
             m.act_forcelimited[h][a] = 0 if fr is None else 1
             m.act_forcerange[h][a][:] = (0.0, 0.0) if fr is None else fr
     set_const(m)
-    pairs = capsule_pairs(bodies, geoms, excludes)
+    pairs = capsule_pairs(bodies, geoms, excludes) if hand_collisions else []
     assert len(pairs) <= abi.MAX_CAPPAIRS
     m.n_cappairs = len(pairs)
     for i, (a, b) in enumerate(pairs):

@@ -149,9 +149,14 @@ typedef struct {
   double energy_penalty_coef;       /* 5e-3 */
   int32_t pgs_iterations;           /* constraint solver sweeps per substep */
   int32_t max_contacts;             /* per env, <= PS_MAX_CONTACTS_LIMIT */
+  int32_t canonical_actions;        /* 1: ps_step actions are in [-1,1] and are rescaled to the
+                                       spec as dm_env_wrappers.CanonicalSpecWrapper does */
 } ps_task_cfg;
 
-#define PS_MAX_CONTACTS_LIMIT 48
+#define PS_MAX_CONTACTS_LIMIT 24
+/* Coupled constraint rows per env (hand limits, contacted-key limits, 4 per contact);
+ * rows beyond this are dropped in order. */
+#define PS_MAX_ROWS 96
 
 /* step_type values (dm_env.StepType) */
 #define PS_FIRST 0
@@ -182,7 +187,7 @@ void ps_destroy(ps_env* env);
  * and writes their first observation into obs[N][obs_dim]. */
 int ps_reset(ps_env* env, const uint8_t* env_mask, float* obs, void* stream);
 
-/* action[N][45] in spec units (CanonicalSpecWrapper already applied). Envs whose
+/* action[N][45] in spec units, or canonical [-1,1] units when cfg.canonical_actions. Envs whose
  * previous step was LAST are reset instead and report PS_FIRST (reward 0, discount 1). */
 int ps_step(ps_env* env, const float* action, float* obs, float* reward, float* discount,
             uint8_t* step_type, void* stream);

@@ -38,7 +38,7 @@
 #define NA PS_HAND_NACT
 #define NV PS_NV
 #define MAXCON PS_MAX_CONTACTS_LIMIT
-#define MAXROW (4 * MAXCON + NH * ND * 2 + NK)
+#define MAXROW (4 * MAXCON + NH * ND * 2 + NK)  /* storage; coupled rows are capped at PS_MAX_ROWS */
 #define MINIMP 0.0001
 #define MAXIMP 0.9999
 #define MINVAL 1e-15
@@ -724,14 +724,15 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
   memset(keyhit, 0, sizeof(keyhit));
   for (int c = 0; c < E->ncon; c++)
     if (E->con[c].kind == 0) keyhit[E->con[c].key] = 1;
-  int nr = 0;
+  int nr = 0, ncoup = 0;  /* coupled rows are capped at PS_MAX_ROWS, later ones dropped */
   for (int h = 0; h < NH; h++)
     for (int j = 0; j < ND; j++) {
       if (!d->dof_limited[h][j]) continue;
       double q = E->q[NK + h * ND + j];
       for (int side = 0; side < 2; side++) {
         double dist = side == 0 ? q - d->dof_range[h][j][0] : d->dof_range[h][j][1] - q;
-        if (dist >= 0.0) continue;
+        if (dist >= 0.0 || ncoup >= PS_MAX_ROWS) continue;
+        ncoup++;
         row* r = &g_rows[nr++];
         memset(r->J, 0, sizeof(r->J));
         r->J[NK + h * ND + j] = side == 0 ? 1.0 : -1.0;
@@ -745,6 +746,10 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       for (int side = 0; side < 2; side++) {
         double dist = side == 0 ? E->q[k] - d->key_range[k][0] : d->key_range[k][1] - E->q[k];
         if (dist >= 0.0) continue;
+        if (pass == 0) {
+          if (ncoup >= PS_MAX_ROWS) continue;
+          ncoup++;
+        }
         row* r = &g_rows[nr++];
         memset(r->J, 0, sizeof(r->J));
         r->J[k] = side == 0 ? 1.0 : -1.0;
@@ -753,6 +758,7 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       }
     }
   for (int c = 0; c < E->ncon; c++) {
+    if (ncoup + 4 > PS_MAX_ROWS) break;  /* whole contacts only */
     contact* cc = &E->con[c];
     double solref[2], solimp[5], mu;
     mix_param(cc->kind == 2 ? &d->hand_contact : &d->piano_contact, &d->hand_contact, solref, solimp, &mu);
@@ -765,6 +771,7 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     else if (cc->kind == 2) tran += d->body_invweight[cc->h1][cc->b1];
     double diag = (1.0 + mu * mu) * tran;
     for (int e = 0; e < 4; e++) {
+      ncoup++;
       row* r = &g_rows[nr++];
       const double* Jt = e < 2 ? Jt1 : Jt2;
       double s = (e & 1) ? -mu : mu;
