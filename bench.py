@@ -1,0 +1,177 @@
+"""Benchmark: env-steps/s of the batched PianoWithShadowHands step on MI355X.
+
+One "step" = one control step (0.05 s of simulated time = 10 physics substeps + task
+layer) of every env on every GPU, random uniform canonical actions (pre-generated on
+device with torch's Philox generator, seed 12345 + rank). Inputs and state are resident in
+HBM when the timed region starts. Multi-GPU: one process per GPU, 4096 envs per GPU
+(weak scaling, envs shard with no data-path collective); episode returns are gathered
+over RCCL after the timed region for logging.
+
+Prints ONE JSON line (rank 0); see DESIGN.md "Measurement".
+"""
+
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+ENVS_PER_GPU = 4096
+# compulsory HBM bytes per env-step (fp32 state, obs 329) - the
+# roofline's algorithmic basis.
+BYTES_PER_ENV_STEP = 4884
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
+    p.add_argument("--song", default="twinkle", choices=["twinkle", "crossing_field", "guren"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-envs", type=int, default=16)
+    p.add_argument("--cpu-sample-steps", type=int, default=300)
+    return p.parse_args()
+
+
+def load_song(dp, name):
+    data = ROOT / "tests" / "data"
+    if name == "twinkle":
+        return dp.music.twinkle_twinkle_little_star_one_hand(), dp.TaskConfig()
+    if name == "crossing_field":
+        return dp.music.parse_midi(data / "Crossing Field Cut 10s.mid"), dp.TaskConfig(trim_silence=True)
+    seq = dp.music.add_fingering_from_annotation_file(data / "Guren no Yumiya Cut 14s.mid",
+                                                      data / "Guren no Yumiya Cut 14s_fingering v3.txt")
+    return seq, dp.TaskConfig(trim_silence=True)
+
+
+def cpu_baseline(dp, seq, task, n_envs, steps):
+    """The fp64 oracle (oracle/pianosim_ref.c), one thread, same song/task, random actions."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import ref  # CPU checker/baseline only
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    env = ref.OracleEnv(md, st, tc, n_envs)
+    env.reset()
+    lo, hi = dp.model.action_spec(md)
+    rng = np.random.RandomState(12345)
+    acts = [rng.uniform(lo, hi, (n_envs, 45)).astype(np.float32) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a in acts:
+        env.step(a)
+    dt = time.perf_counter() - t0
+    return {"value": n_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_envs} envs x {steps} random-action control steps, {dt:.1f} s, 1 thread "
+                      f"(fp64 oracle restatement; MuJoCo/dm_control absent)"}
+
+
+def pmc_traffic(n_envs):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if it matches."""
+    f = ROOT / "profiles" / "pmc_latest.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        if d.get("envs") == n_envs:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    dp = importlib.import_module("diffusion-piano_amd")
+    seq, task = load_song(dp, args.song)
+    env = dp.BatchedPianoEnv(args.envs, seq, task, device=dev, seed=rank)
+    N = args.envs
+    gen = torch.Generator(device=dev).manual_seed(12345 + rank)
+    pool = max(1, min(args.steps + args.warmup, 64))
+    actions = [torch.rand(N, 45, device=dev, generator=gen) * 2 - 1 for _ in range(pool)]
+    env.reset()
+    ep_ret = torch.zeros(N, device=dev)
+    for i in range(args.warmup):
+        env.step(actions[i % pool])
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record()
+        _, rew, _, _ = env.step(actions[(args.warmup + i) % pool])
+        ends[i].record()
+        ep_ret += rew
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # logging only: RCCL all-gather of the per-env returns over xGMI
+        allret = [torch.empty_like(ep_ret) for _ in range(world)]
+        dist.all_gather(allret, ep_ret)
+        mean_ret = float(torch.cat(allret).mean())
+    else:
+        mean_ret = float(ep_ret.mean())
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    total_steps = N * world * args.steps
+    value = total_steps / elapsed
+    if rank == 0:
+        achieved = BYTES_PER_ENV_STEP * N / (kernel_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(N)
+        line = {
+            "metric": "env steps/sec at 4096 parallel envs",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: uniform random canonical actions (torch Philox, seed 12345+rank)",
+            "config": {"workload": f"{N} envs/GPU {args.song} random-action rollout, 10 physics substeps "
+                                   f"per env-step, PGS {task.pgs_iterations} sweeps",
+                       "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
+                       "mean_return_logged": mean_ret},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
+                         "bytes_per_env_step": BYTES_PER_ENV_STEP},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(dp, seq, task, args.cpu_sample_envs, args.cpu_sample_steps)
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,7 +8,7 @@ import os
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "libpianosim.so"
+LIB_PATH = Path(os.environ.get("PIANOSIM_LIB", HERE / "libpianosim.so"))
 
 # Every entry point declared in include/pianosim.h.
 EXPORTS = (

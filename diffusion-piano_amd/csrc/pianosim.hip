@@ -16,6 +16,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -148,6 +149,7 @@ struct Song {
 struct Cfg {
   int lookahead, fingering, forearm, wrong_press, pgs_iter, maxcon, obs_dim, canonical;
   float energy_coef;
+  int skip;  // development ablation mask (PIANOSIM_SKIP env var); 0 in production
 };
 
 struct Bufs {
@@ -1148,6 +1150,25 @@ __device__ __forceinline__ bool key_active(const Work& W, int k) {
   return (W.act_bits[k >> 5] >> (k & 31)) & 1;
 }
 
+// ------------------------------------------------------------------ diagnostic phase timing
+// Built only with -DPS_TIMING (libpianosim_timing.so): per-phase s_memtime deltas summed
+// per env into a debug buffer. The production library contains none of this.
+#ifdef PS_TIMING
+#define NPHASE 12
+#define TSTAMP(slot)                                                      \
+  do {                                                                    \
+    __syncthreads();                                                      \
+    uint64_t t_ = __builtin_amdgcn_s_memtime();                          \
+    tacc[slot] += t_ - tlast;                                             \
+    tlast = t_;                                                           \
+  } while (0)
+__device__ uint64_t* g_timing = nullptr;
+#else
+#define TSTAMP(slot) \
+  do {               \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------ the kernel
 __global__ void __launch_bounds__(64) pianosim_kernel(const DevModel* __restrict__ m, Song song, Cfg cfg, Bufs bufs,
                                                       const float* __restrict__ action, const uint8_t* __restrict__ mask,
@@ -1215,17 +1236,34 @@ __global__ void __launch_bounds__(64) pianosim_kernel(const DevModel* __restrict
   if (lane == 0) W.sustain = cfg.canonical ? (a_e[NU] + 1.f) * 0.5f : a_e[NU];
   __syncthreads();
   // ---- physics substeps
+#ifdef PS_TIMING
+  uint64_t tacc[NPHASE] = {0};
+  uint64_t tlast = __builtin_amdgcn_s_memtime();
+#endif
   for (int s = 0; s < m->nsub; s++) {
-    kinematics(m, W, lane);
-    dynamics(m, W, applied, lane);
-    collide(m, W, cfg.maxcon, lane);
-    factor(m, W, lane);
+    if (!(cfg.skip & 1)) kinematics(m, W, lane);
+    TSTAMP(0);
+    if (!(cfg.skip & 2)) dynamics(m, W, applied, lane);
+    TSTAMP(1);
+    if (!(cfg.skip & 4)) collide(m, W, cfg.maxcon, lane);
+    else if (lane == 0) W.ncon = 0;
+    TSTAMP(2);
+    if (!(cfg.skip & 8)) factor(m, W, lane);
+    TSTAMP(3);
     for (int i = lane; i < NV; i += 64) W.qas[i] = W.qfs[i];
     __syncthreads();
-    solve<false>(m, W, W.qas, lane);
+    if (!(cfg.skip & 16)) solve<false>(m, W, W.qas, lane);
     __syncthreads();
-    constraints(m, W, MAXROW, lane);
-    solve_and_integrate(m, W, cfg.pgs_iter, lane);
+    TSTAMP(4);
+    if (!(cfg.skip & 32)) constraints(m, W, MAXROW, lane);
+    else if (lane == 0) W.nrow = 0;
+    __syncthreads();
+    TSTAMP(5);
+    solve_and_integrate(m, W, (cfg.skip & 64) ? 0 : cfg.pgs_iter, lane);
+    TSTAMP(6);
+#ifdef PS_TIMING
+    if (lane == 0) { tacc[9] += W.nrow; tacc[10] += W.ncon; }
+#endif
   }
   // ---- mj_step1 at the final state + task layer
   kinematics(m, W, lane);
@@ -1309,6 +1347,11 @@ __global__ void __launch_bounds__(64) pianosim_kernel(const DevModel* __restrict
   float disc = 1.f;
   if (!terminal && cfg.wrong_press && failure) { terminal = true; disc = 0.f; }
   write_obs(m, song, cfg, W, t_new < song.T ? t_new : t_new - 1, obs_e, lane);
+  TSTAMP(7);
+#ifdef PS_TIMING
+  if (lane == 0 && g_timing)
+    for (int i = 0; i < NPHASE; i++) g_timing[(size_t)e * NPHASE + i] += tacc[i];
+#endif
   // ---- write back
   for (int i = lane; i < NV; i += 64) {
     bufs.qpos[(size_t)e * NV + i] = W.q[i];
@@ -1666,7 +1709,8 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
   Song song{E->T, E->d_goal, E->d_count, E->d_keys, E->d_fingers};
   Cfg cfg{E->cfg.n_steps_lookahead, E->cfg.fingering_reward, E->cfg.forearm_reward, E->cfg.wrong_press_termination,
           E->cfg.pgs_iterations, E->cfg.max_contacts, E->obs_dim, E->cfg.canonical_actions,
-          (float)E->cfg.energy_penalty_coef};
+          (float)E->cfg.energy_penalty_coef, 0};
+  if (const char* sk = getenv("PIANOSIM_SKIP")) cfg.skip = atoi(sk);
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon};
   hipLaunchKernelGGL(pianosim_kernel, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b, action,
@@ -1741,6 +1785,27 @@ int ps_fingertips(ps_env* E, float* xpos, void* stream) {
                         (hipStream_t)stream));
   return 0;
 }
+
+#ifdef PS_TIMING
+// diagnostic: per-env phase cycle sums [n][NPHASE] since the last call (host buffer)
+int ps_debug_timing(ps_env* E, uint64_t* out) {
+  static uint64_t* d = nullptr;
+  static size_t cap = 0;
+  size_t bytes = sizeof(uint64_t) * E->n * NPHASE;
+  if (cap < bytes) {
+    if (d) (void)hipFree(d);
+    HIPCHK(hipMalloc(&d, bytes));
+    cap = bytes;
+    HIPCHK(hipMemset(d, 0, bytes));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_timing), &d, sizeof(d)));
+    return 0;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  if (out) HIPCHK(hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(d, 0, bytes));
+  return 0;
+}
+#endif
 
 int ps_contact_count(ps_env* E, int32_t* ncon, void* stream) {
   if (!E || !ncon) return fail("null argument");

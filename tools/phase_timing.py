@@ -1,0 +1,27 @@
+"""Per-phase cycle breakdown from the -DPS_TIMING diagnostic build (run with
+PIANOSIM_LIB=diffusion-piano_amd/libpianosim_timing.so). Shares, not absolute speed."""
+import ctypes as C, importlib, sys
+from pathlib import Path
+import numpy as np, torch
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT)); sys.path.insert(0, str(ROOT / "tests"))
+dp = importlib.import_module("diffusion-piano_amd")
+lib = importlib.import_module("diffusion-piano_amd._lib")
+from helpers import song
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+L = lib.load()
+L.ps_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
+g = dp.BatchedPianoEnv(N, song(dp, "twinkle"), dp.TaskConfig(), device="cuda:0")
+g.reset()
+L.ps_debug_timing(g._h, None)
+gen = torch.Generator(device="cuda:0").manual_seed(1)
+for i in range(10):
+    g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
+out = np.zeros((N, 12), np.uint64)
+L.ps_debug_timing(g._h, out.ctypes.data)
+names = ["kinematics", "dynamics", "collide", "factor", "solve_smooth", "constraints", "pgs+integrate", "final+task"]
+tot = out[:, :8].astype(np.float64).sum(axis=1)
+for i, n in enumerate(names):
+    v = out[:, i].astype(np.float64)
+    print(f"{n:14s} {v.mean()/10:12.0f} cycles/env-step  {100*v.sum()/tot.sum():5.1f}%")
+print(f"total {tot.mean()/10:.0f} cycles/env-step per wave; mean rows/substep {out[:,9].mean()/100:.1f} mean contacts {out[:,10].mean()/100:.2f}")
