@@ -729,7 +729,7 @@ __device__ void row_scalars(const DevModel* __restrict__ m, Work& W, int r, floa
     W.r_b[r] = jqs - aref;
     W.r_R[r] = R;
     W.r_arinv[r] = 1.f / (A + R);
-    W.r_f[r] = fmaxf(0.f, -(jws - aref) / R);
+    W.r_f[r] = 0.f;  // cold start: a qacc_warmstart-derived start is unstable for new stiff contacts
   }
 }
 

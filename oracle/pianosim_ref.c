@@ -15,8 +15,8 @@
  *     kinematics, composite-rigid-body mass matrix + armature, tree LDL (mj_factorI /
  *     mj_solveLD), recursive Newton-Euler bias, passive spring/damper, position
  *     actuators (joint + fixed tendon), collision, soft constraints (solref/solimp,
- *     refsafe), pyramidal friction cones, PGS dual solve warm-started from
- *     qacc_warmstart, Euler with implicit joint damping (mj_EulerSkip).
+ *     refsafe), pyramidal friction cones, PGS dual solve (cold start, fixed sweeps),
+ *     Euler with implicit joint damping (mj_EulerSkip).
  * Parity status: the task layer is pinned by the reference tests' known answers and the
  * golden song fixtures (tests/golden/); the physics is "parity unpinned" against MuJoCo
  * (no mujoco/dm_control/Menagerie in this container, no reference test records numeric
@@ -787,7 +787,10 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
   for (int i = 0; i < nr; i++) {
     row* r = &g_rows[i];
     if (r->closed) { r->f = fmax(0.0, -r->b / (r->Aii + r->R)); continue; }
-    r->f = fmax(0.0, -(dotv(r->J, E->qacc_ws) - r->aref) / r->R);
+    /* cold start: a qacc_warmstart-derived start (f = -D(J qacc_ws - aref)) is unsafe for
+     * contacts that appeared this substep (huge forces where R is small); MuJoCo guards it
+     * with a cost comparison, here the dual starts at 0 (always stable). */
+    r->f = 0.0;
     for (int k = 0; k < NV; k++) w[k] += r->y[k] * r->f;
   }
   for (int it = 0; it < cfg->pgs_iterations; it++) {
