@@ -16,7 +16,7 @@ NACTION = NU + 1
 MAX_CAPPAIRS = 768
 MAX_NOTES = 16
 MAX_CONTACTS_LIMIT = 24
-MAX_ROWS = 96
+MAX_ROWS = 64
 NTERMS = 5
 FIRST, MID, LAST = 0, 1, 2
 

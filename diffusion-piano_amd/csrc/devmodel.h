@@ -74,6 +74,12 @@ struct DevModel {
   int pair[PS_MAX_CAPPAIRS][2];
   // triangular (a,b) table for the LDL update
   int tri_a[NTRI + 8], tri_b[NTRI + 8];
+  // v2 lane-owned topology (packed, loaded into registers once per launch)
+  int body_level[NBT];
+  int body_child_pack[NBT];   // up to 5 children, 6 bits each (child global body index)
+  int dof_anc_pack[NDT][3];   // anc[1..8] as bytes (255 = none): [0]=anc1..4, [1]=anc5..8
+  float key_top_zmax;         // max over keys of (z + half_z) + 0.02 : capsule z prefilter
+  float piano_xmin, piano_xmax;  // x extent of keys (+0.02) and base for the x prefilter
 };
 
 }  // namespace ps

@@ -156,7 +156,7 @@ typedef struct {
 #define PS_MAX_CONTACTS_LIMIT 24
 /* Coupled constraint rows per env (hand limits, contacted-key limits, 4 per contact);
  * rows beyond this are dropped in order. */
-#define PS_MAX_ROWS 96
+#define PS_MAX_ROWS 64
 
 /* step_type values (dm_env.StepType) */
 #define PS_FIRST 0

@@ -701,6 +701,8 @@ static void mix_param(const ps_contact_param* a, const ps_contact_param* b, doub
 
 static _Thread_local row g_rows[MAXROW];
 int ref_debug_level = 0;
+long ref_rows_hist[PS_MAX_ROWS + 2];
+long ref_con_hist[PS_MAX_CONTACTS_LIMIT + 2];
 #include <stdio.h>
 
 static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
@@ -781,6 +783,8 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     }
   }
 
+  ref_rows_hist[ncoup]++;
+  ref_con_hist[E->ncon]++;
   /* PGS on the coupled rows; closed-form free key rows */
   double w[NV];
   memset(w, 0, sizeof(w));

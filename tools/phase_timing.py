@@ -19,8 +19,8 @@ for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
 out = np.zeros((N, 12), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
-names = ["kinematics", "dynamics", "collide", "factor", "solve_smooth", "constraints", "pgs+integrate", "final+task"]
-tot = out[:, :8].astype(np.float64).sum(axis=1)
+names = ["kinematics", "dynamics", "collide", "factor", "solve_smooth", "constraints", "integrate", "final+task", "pgs"]
+tot = out[:, :9].astype(np.float64).sum(axis=1)
 for i, n in enumerate(names):
     v = out[:, i].astype(np.float64)
     print(f"{n:14s} {v.mean()/10:12.0f} cycles/env-step  {100*v.sum()/tot.sum():5.1f}%")
