@@ -26,9 +26,15 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 ENVS_PER_GPU = 4096
-# compulsory HBM bytes per env-step (fp32 state, obs 329) - the
-# roofline's algorithmic basis.
-BYTES_PER_ENV_STEP = 4884
+METRIC = "env steps/sec at 4096 parallel envs; qpos L\u221e drift vs CPU MuJoCo"
+
+
+def bytes_per_env_step(obs_dim):
+    """compulsory HBM bytes per env-step, the roofline's algorithmic basis:
+    action 45x4 + (qpos, qvel, qacc_warmstart) 140x4 read+write + sustain/t_idx 16
+    + obs write + reward/discount/step_type 12 = 4884 B (obs 329) / 4844 B (obs 319)."""
+    return 45 * 4 + 3 * 140 * 4 * 2 + 16 + obs_dim * 4 + 12
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -38,10 +44,10 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
-    p.add_argument("--song", default="twinkle", choices=["twinkle", "crossing_field", "guren"])
+    p.add_argument("--song", default="crossing_field", choices=["twinkle", "crossing_field", "guren"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-envs", type=int, default=16)
-    p.add_argument("--cpu-sample-steps", type=int, default=300)
+    p.add_argument("--cpu-sample-steps", type=int, default=1000)
     return p.parse_args()
 
 
@@ -75,18 +81,34 @@ def cpu_baseline(dp, seq, task, n_envs, steps):
                       f"(fp64 oracle restatement; MuJoCo/dm_control absent)"}
 
 
-def pmc_traffic(n_envs):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if it matches."""
-    f = ROOT / "profiles" / "pmc_latest.json"
-    if not f.exists():
-        return None
+def _profile(name):
+    f = ROOT / "profiles" / name
     try:
-        d = json.loads(f.read_text())
-        if d.get("envs") == n_envs:
-            return d.get("hbm_bytes_per_launch")
-    except Exception:
-        pass
+        return json.loads(f.read_text()) if f.exists() else None
+    except ValueError:
+        return None
+
+
+def pmc_traffic(n_envs, song):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if it matches."""
+    d = _profile("pmc_latest.json")
+    if d and d.get("envs") == n_envs and d.get("song", song) == song:
+        return d.get("hbm_bytes_per_launch")
     return None
+
+
+def drift_summary():
+    """qpos L-inf drift vs the fp64 CPU step, from the committed drift report written by
+    tests/test_gpu_drift.py (PIANOSIM_REPORT=profiles/drift_latest.json)."""
+    d = _profile("drift_latest.json")
+    if not d:
+        return None
+    out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"), "song": d.get("song")}
+    for k in ("zero_action", "trace_actions", "random_actions"):
+        if k in d:
+            out[k] = {"teacher_forced_p99": d[k]["teacher_forced_qpos_linf"]["p99"],
+                      "free_running_1000_steps_max": d[k]["free_running_max_over_1000"]}
+    return out
 
 
 def main():
@@ -141,10 +163,11 @@ def main():
     total_steps = N * world * args.steps
     value = total_steps / elapsed
     if rank == 0:
-        achieved = BYTES_PER_ENV_STEP * N / (kernel_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(N)
+        bpe = bytes_per_env_step(env.obs_dim)
+        achieved = bpe * N / (kernel_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(N, args.song)
         line = {
-            "metric": "env steps/sec at 4096 parallel envs",
+            "metric": METRIC,
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -163,7 +186,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
-                         "bytes_per_env_step": BYTES_PER_ENV_STEP},
+                         "bytes_per_env_step": bpe},
+            "qpos_drift": drift_summary(),
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(dp, seq, task, args.cpu_sample_envs, args.cpu_sample_steps)

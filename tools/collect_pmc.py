@@ -1,6 +1,6 @@
 """Summarise rocprofv3 outputs for pianosim_kernel into profiles/.
 
-usage: python tools/collect_pmc.py <trace_dir> <fetch_dir> <write_dir> <envs> <out_prefix>
+usage: python tools/collect_pmc.py <trace_dir> <fetch_dir> <write_dir> <envs> <song> <out_prefix> [warmup]
 
 * <trace_dir>: `rocprofv3 --kernel-trace --stats --output-format csv` of bench.py
 * <fetch_dir>/<write_dir>: separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes
@@ -35,20 +35,33 @@ def counter(d, name):
 
 
 def main():
-    tdir, fdir, wdir, envs, prefix = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    tdir, fdir, wdir, envs, song, prefix = sys.argv[1:4] + [int(sys.argv[4])] + sys.argv[5:7]
+    warmup = int(sys.argv[7]) if len(sys.argv) > 7 else 5
     stats = [r for r in rows(tdir, "*kernel_stats.csv") if "pianosim_kernel" in r.get("Name", "")]
     fetch_kb = counter(fdir, "FETCH_SIZE")
     write_kb = counter(wdir, "WRITE_SIZE")
-    out = {"envs": envs, "kernel": "pianosim_kernel"}
+    out = {"envs": envs, "song": song, "kernel": "pianosim_kernel"}
     if stats:
         s = stats[0]
-        out["rocprof_avg_ns"] = float(s.get("AverageNs", 0))
+        out["rocprof_avg_ns_all_launches"] = float(s.get("AverageNs", 0))
         out["rocprof_calls"] = int(s.get("Calls", 0))
+    # the timed steps only: bench.py launches reset (1) + warmup (5) before the timed region
+    tr = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows(tdir, "*kernel_trace.csv")
+                if "pianosim_kernel" in r.get("Kernel_Name", ""))
+    timed = [e - b for b, e in tr[1 + warmup:]]
+    if timed:
+        out["rocprof_avg_ns"] = sum(timed) / len(timed)
+        out["rocprof_timed_launches"] = len(timed)
     if fetch_kb is not None and write_kb is not None:
         out["fetch_kb_per_launch"] = fetch_kb
         out["write_kb_per_launch"] = write_kb
         out["hbm_bytes_per_launch"] = (2.0 * fetch_kb + write_kb) * 1024.0
     Path("profiles").mkdir(exist_ok=True)
+    if stats:
+        with open(f"profiles/{prefix}_kernel_stats.csv", "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(stats[0].keys()))
+            w.writeheader()
+            w.writerows(rows(tdir, "*kernel_stats.csv"))
     Path(f"profiles/{prefix}_pmc.json").write_text(json.dumps(out, indent=1))
     Path("profiles/pmc_latest.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out))

@@ -1,0 +1,37 @@
+"""Quick GPU throughput sweep over env counts and songs (development aid; bench.py is the
+contract). usage: python tools/throughput.py [song] [N ...]"""
+import importlib
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+dp = importlib.import_module("diffusion-piano_amd")
+from helpers import song  # noqa: E402
+
+
+def throughput(name, n, steps=20):
+    task = dp.TaskConfig(trim_silence=name != "twinkle")
+    g = dp.BatchedPianoEnv(n, song(dp, name), task, device="cuda:0")
+    g.reset()
+    gen = torch.Generator(device="cuda:0").manual_seed(12345)
+    acts = [torch.rand(n, 45, device="cuda:0", generator=gen) * 2 - 1 for _ in range(steps)]
+    for i in range(3):
+        g.step(acts[i])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        g.step(acts[i])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"{name:15s} N={n:6d}: {n * steps / dt:12,.0f} env-steps/s ({dt / steps * 1e3:.2f} ms/step)", flush=True)
+
+
+if __name__ == "__main__":
+    name = sys.argv[1] if len(sys.argv) > 1 else "twinkle"
+    for n in [int(x) for x in sys.argv[2:]] or [1024, 4096, 16384]:
+        throughput(name, n)
