@@ -26,7 +26,10 @@ constexpr int MAXCHILD = 5;
 constexpr int MAXCON = 24;     // per-env contact capacity of the GPU workspace
 constexpr int MAXROW = PS_MAX_ROWS;
 constexpr int KEYLANE = 52;    // lane that carries a row's key-dof entry
-constexpr int ROWSTRIDE = 53;  // 52 hand dofs + key entry; odd stride: conflict-free columns
+// Constraint rows y = L^-T J^T are stored compressed: a row touches the ancestor chains of
+// at most two hand bodies (<= 2 * MAXDEP hand dofs, in r_mask bit order) plus one key.
+constexpr int YS = 20;         // row stride: 18 hand slots, [YKEY] = key entry, 1 pad
+constexpr int YKEY = 19;
 constexpr int NTRI = MAXDEP * (MAXDEP - 1) / 2;  // (a,b) pairs 1<=a<=b<=8
 
 struct DevModel {

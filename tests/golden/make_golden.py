@@ -17,7 +17,7 @@ trim_silence window (note_seq is absent); those inputs are produced by this repo
 parser (``music.parse_midi`` / ``music.trim_silence``) and the reference trajectory code
 is run on them. The fixtures record which input path was used.
 
-Usage: python tools/make_golden.py  (writes tests/golden/*.json)
+Usage: python tests/golden/make_golden.py  (writes tests/golden/*.json)
 """
 
 from __future__ import annotations
@@ -31,7 +31,7 @@ from pathlib import Path
 import numpy as np
 
 REF = Path("/root/reference")
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 OUT = ROOT / "tests" / "golden"
 sys.path.insert(0, str(ROOT / "diffusion-piano_amd"))
 import music as our_music  # noqa: E402  (only for the .mid parse, see module docstring)
