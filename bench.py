@@ -124,14 +124,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     dp = importlib.import_module("diffusion-piano_amd")
+    sharding = importlib.import_module("diffusion-piano_amd.sharding")
     seq, task = load_song(dp, args.song)
-    env = dp.BatchedPianoEnv(args.envs, seq, task, device=dev, seed=rank)
-    N = args.envs
+    shard = sharding.shard_envs(args.envs * world, rank, world)  # weak scaling: envs per GPU fixed
+    env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=shard.start)
+    N = shard.count
     gen = torch.Generator(device=dev).manual_seed(12345 + rank)
     pool = max(1, min(args.steps + args.warmup, 64))
     actions = [torch.rand(N, 45, device=dev, generator=gen) * 2 - 1 for _ in range(pool)]
     env.reset()
-    ep_ret = torch.zeros(N, device=dev)
+    returns = sharding.EpisodeReturns(N, dev)
     for i in range(args.warmup):
         env.step(actions[i % pool])
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -142,25 +144,18 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record()
-        _, rew, _, _ = env.step(actions[(args.warmup + i) % pool])
+        _, rew, _, st = env.step(actions[(args.warmup + i) % pool])
         ends[i].record()
-        ep_ret += rew
+        returns.update(rew, st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # logging only: RCCL all-gather of the per-env returns over xGMI
-        allret = [torch.empty_like(ep_ret) for _ in range(world)]
-        dist.all_gather(allret, ep_ret)
-        mean_ret = float(torch.cat(allret).mean())
-    else:
-        mean_ret = float(ep_ret.mean())
+    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
+    # logging only: RCCL all-gather of the episode returns over xGMI, after the timed region
+    fin_sum, fin_n, run_sum, n_all = returns.gather()
+    mean_ret = run_sum / n_all
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
-    total_steps = N * world * args.steps
+    total_steps = args.envs * world * args.steps
     value = total_steps / elapsed
     if rank == 0:
         bpe = bytes_per_env_step(env.obs_dim)
@@ -182,7 +177,7 @@ def main():
             "config": {"workload": f"{N} envs/GPU {args.song} random-action rollout, 10 physics substeps "
                                    f"per env-step, PGS {task.pgs_iterations} sweeps",
                        "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
-                       "mean_return_logged": mean_ret},
+                       "mean_return_logged": mean_ret, "episodes_finished": fin_n},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,

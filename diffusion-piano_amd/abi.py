@@ -74,6 +74,23 @@ class SongDesc(C.Structure):
     _fields_ = [("T", i32), ("goal", C.POINTER(C.c_float)), ("count", C.POINTER(i32)),
                 ("keys", C.POINTER(i32)), ("fingers", C.POINTER(i32))]
 
+    @classmethod
+    def from_tables(cls, song) -> "SongDesc":
+        """ps_song_desc over a music.SongTables; the contiguous host copies are kept alive on
+        the returned struct (ps_create copies them to the device)."""
+        import numpy as np
+
+        sd = cls()
+        sd._arrays = (np.ascontiguousarray(song.goal, np.float32), np.ascontiguousarray(song.count, np.int32),
+                      np.ascontiguousarray(song.keys, np.int32), np.ascontiguousarray(song.fingers, np.int32))
+        goal, count, keys, fingers = sd._arrays
+        sd.T = int(song.T)
+        sd.goal = goal.ctypes.data_as(C.POINTER(C.c_float))
+        sd.count = count.ctypes.data_as(C.POINTER(i32))
+        sd.keys = keys.ctypes.data_as(C.POINTER(i32))
+        sd.fingers = fingers.ctypes.data_as(C.POINTER(i32))
+        return sd
+
 
 class TaskCfg(C.Structure):
     _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),

@@ -171,16 +171,7 @@ class BatchedPianoEnv:
         self.obs_slices = obs_layout(self.task_cfg)
         self.action_lo, self.action_hi = model_lib.action_spec(self.model_desc)
         L = _lib.load()
-        self._goal = np.ascontiguousarray(self.song.goal, np.float32)
-        self._count = np.ascontiguousarray(self.song.count, np.int32)
-        self._keys = np.ascontiguousarray(self.song.keys, np.int32)
-        self._fingers = np.ascontiguousarray(self.song.fingers, np.int32)
-        sd = abi.SongDesc()
-        sd.T = self.song.T
-        sd.goal = self._goal.ctypes.data_as(C.POINTER(C.c_float))
-        sd.count = self._count.ctypes.data_as(C.POINTER(C.c_int32))
-        sd.keys = self._keys.ctypes.data_as(C.POINTER(C.c_int32))
-        sd.fingers = self._fingers.ctypes.data_as(C.POINTER(C.c_int32))
+        sd = abi.SongDesc.from_tables(self.song)
         if L.ps_model_desc_size() != C.sizeof(abi.ModelDesc):
             raise _lib.PianosimError("ps_model_desc layout mismatch between abi.py and the library")
         h = C.c_void_p()

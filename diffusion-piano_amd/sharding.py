@@ -1,0 +1,87 @@
+"""Env sharding across GPUs (one process per GPU) and the logging-only collectives.
+
+Envs are independent units: global env ``g`` lives on rank
+``g // envs_per_rank`` at local index ``g % envs_per_rank``; ``step()`` has no exchange
+step. The only collectives are off the data path, for logging: the max of a wall time over
+ranks (benchmark) and an all-gather of finished-episode returns - RCCL over xGMI on the GPU
+node (backend "nccl"), gloo in the CPU tests. The reference's serial VecEnv
+(parallelized_base_v2.py:53-60) has no counterpart of either.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class EnvShard:
+    rank: int
+    world: int
+    start: int   # first global env id on this rank
+    count: int   # envs on this rank
+
+    @property
+    def stop(self) -> int:
+        return self.start + self.count
+
+
+def shard_envs(total: int, rank: int, world: int) -> EnvShard:
+    """Contiguous, balanced split of ``total`` envs over ``world`` ranks (sizes differ by <= 1)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    if total < world:
+        raise ValueError(f"{total} envs cannot be spread over {world} ranks")
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return EnvShard(rank, world, start, base + (1 if rank < extra else 0))
+
+
+class EpisodeReturns:
+    """Per-env running returns on the env's device; finished episodes (step_type LAST)
+    are appended to a device-side log without a host sync per step."""
+
+    def __init__(self, num_envs: int, device):
+        import torch
+
+        self._torch = torch
+        self.running = torch.zeros(num_envs, device=device, dtype=torch.float64)
+        self.finished_sum = torch.zeros((), device=device, dtype=torch.float64)
+        self.finished_count = torch.zeros((), device=device, dtype=torch.int64)
+
+    def update(self, reward, step_type) -> None:
+        """Call after every step: FIRST steps (reward 0 after auto-reset) start a new
+        episode, LAST steps close one."""
+        torch = self._torch
+        first = step_type == 0
+        self.running = torch.where(first, torch.zeros_like(self.running), self.running + reward.to(torch.float64))
+        last = step_type == 2
+        self.finished_sum += torch.where(last, self.running, torch.zeros_like(self.running)).sum()
+        self.finished_count += last.sum()
+
+    def gather(self, group=None):
+        """All ranks: (sum of finished returns, number of finished episodes, sum of the
+        running returns, number of envs) over the whole job."""
+        import torch
+        import torch.distributed as dist
+
+        local = torch.stack([self.finished_sum, self.finished_count.to(torch.float64),
+                             self.running.sum(), torch.tensor(float(self.running.numel()),
+                                                              device=self.running.device, dtype=torch.float64)])
+        if dist.is_available() and dist.is_initialized():
+            parts = [torch.empty_like(local) for _ in range(dist.get_world_size(group))]
+            dist.all_gather(parts, local, group=group)
+            local = torch.stack(parts).sum(0)
+        s, n, rs, ne = (float(x) for x in local.cpu())
+        return s, int(n), rs, int(ne)
+
+
+def max_over_ranks(value: float, device=None, group=None) -> float:
+    """Max of a host scalar over ranks (identity when not distributed)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(value)
+    t = torch.tensor([float(value)], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
