@@ -57,6 +57,7 @@ struct DevModel {
   float dof_axis[NDT][3], dof_lo[NDT], dof_hi[NDT], dof_damp[NDT], dof_arm[NDT], dof_dinv[NDT];
   int dof_depth[NDT], dof_anc[NDT][MAXDEP];
   uint64_t dof_ancmask[NDT];
+  uint64_t dof_descmask[NDT];  // bit g: hand dof g is a proper descendant
   int dof_ndesc[NDT], dof_desc[NDT][ND];
   int ndepth, dep_start[MAXDEP + 1], dep_dof[NDT];
   int dof_act[NDT];          // actuator driving the dof (global index) or -1

@@ -188,6 +188,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     for (int a = 1; a <= m->dof_depth[g]; a++) {
       int i = m->dof_anc[g][a];
       m->dof_desc[i][m->dof_ndesc[i]++] = g;
+      m->dof_descmask[i] |= 1ull << g;
     }
   m->ndepth = maxdep + 1;
   n = 0;

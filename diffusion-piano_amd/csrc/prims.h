@@ -253,6 +253,24 @@ __device__ void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3* c1, f3* c2) {
   *c2 = p2 + d2 * t;
 }
 
+// sin/cos for the joint-angle range (|x| << 1e4): Cody-Waite reduction by pi/2 and the
+// Cephes minimax polynomials on [-pi/4, pi/4] (~1 ulp); no table loads, no slow path.
+__device__ __forceinline__ void fsincos(float x, float* sp, float* cp) {
+  const float k = rintf(x * 0.636619772367581343f);
+  float r = fmaf(-k, 1.57079637050628662f, x);
+  r = fmaf(-k, -4.37113900018624283e-8f, r);
+  const float z = r * r;
+  const float sn = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  const float cs = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                        fmaf(-0.5f, z, 1.f));
+  const int q = (int)k & 3;
+  float s = (q & 1) ? cs : sn, c = (q & 1) ? sn : cs;
+  if (q == 1 || q == 2) c = -c;
+  if (q & 2) s = -s;
+  *sp = s;
+  *cp = c;
+}
+
 __device__ __forceinline__ float impedance(const float* si, float pos) {
   float d0 = clampf(si[0], MINIMP, MAXIMP), dw = clampf(si[1], MINIMP, MAXIMP);
   float width = si[2], mid = si[3], power = si[4];
@@ -261,6 +279,7 @@ __device__ __forceinline__ float impedance(const float* si, float pos) {
   else {
     float y;
     if (power == 1.f) y = x;
+    else if (power == 2.f) y = x <= mid ? x * x / mid : 1.f - (1.f - x) * (1.f - x) / (1.f - mid);
     else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
     else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
     imp = d0 + y * (dw - d0);

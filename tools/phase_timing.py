@@ -17,11 +17,14 @@ L.ps_debug_timing(g._h, None)
 gen = torch.Generator(device="cuda:0").manual_seed(1)
 for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
-out = np.zeros((N, 12), np.uint64)
+out = np.zeros((N, 16), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
-names = ["kinematics", "dynamics", "collide", "factor", "solve_smooth", "constraints", "integrate", "final+task", "pgs"]
-tot = out[:, :9].astype(np.float64).sum(axis=1)
-for i, n in enumerate(names):
+names = {0: "kinematics", 1: "dynamics", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
+         3: "factor", 4: "solve_smooth",
+         12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T", 15: "cons:finish",
+         8: "pgs", 6: "integrate"}
+tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
+for i, n in names.items():
     v = out[:, i].astype(np.float64)
     print(f"{n:14s} {v.mean()/10:12.0f} cycles/env-step  {100*v.sum()/tot.sum():5.1f}%")
 print(f"total {tot.mean()/10:.0f} cycles/env-step per wave; mean rows/substep {out[:,9].mean()/100:.1f} mean contacts {out[:,10].mean()/100:.2f}")
