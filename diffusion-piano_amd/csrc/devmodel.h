@@ -31,6 +31,8 @@ constexpr int KEYLANE = 52;    // lane that carries a row's key-dof entry
 constexpr int YS = 20;         // row stride: 18 hand slots, [YKEY] = key entry, 1 pad
 constexpr int YKEY = 19;
 constexpr int NTRI = MAXDEP * (MAXDEP - 1) / 2;  // (a,b) pairs 1<=a<=b<=8
+constexpr int NKB = 64;        // key-range buckets along y
+constexpr int KGEO = 16;       // floats per key collision record
 
 struct DevModel {
   float timestep;
@@ -84,6 +86,14 @@ struct DevModel {
   int dof_anc_pack[NDT][3];   // anc[1..8] as bytes (255 = none): [0]=anc1..4, [1]=anc5..8
   float key_top_zmax;         // max over keys of (z + half_z) + 0.02 : capsule z prefilter
   float piano_xmin, piano_xmax;  // x extent of keys (+0.02) and base for the x prefilter
+  // key range of a y interval: NKB buckets over the keys' y extent, kb_first[b] = first key
+  // with yhi >= bucket start, kb_end[b] = first key with ylo > bucket end (conservative)
+  float kb_y0, kb_inv;
+  uint8_t kb_first[NKB], kb_end[NKB];
+  int npairs_same;            // leading capsule pairs within one hand (the rest cross hands)
+  // per-key collision record, staged into LDS by collide2: pos(3) half(3) anchor(3), then the
+  // conservative AABB of the key box over its joint range: xlo xhi ylo yhi ztop, pad
+  alignas(16) float key_geo[NK][KGEO];
 };
 
 }  // namespace ps

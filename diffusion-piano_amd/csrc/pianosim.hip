@@ -286,6 +286,32 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     m->piano_xmin = xmin;
     m->piano_xmax = xmax;
   }
+  for (int k = 0; k < NK; k++) {
+    float* g = m->key_geo[k];
+    for (int i = 0; i < 3; i++) { g[i] = m->key_pos[k][i]; g[3 + i] = m->key_half[k][i]; g[6 + i] = m->key_anchor[k][i]; }
+    g[9] = m->key_pos[k][0] - m->key_half[k][0] - 0.02f;
+    g[10] = m->key_pos[k][0] + m->key_half[k][0] + 0.02f;
+    g[11] = m->key_ylo[k];
+    g[12] = m->key_yhi[k];
+    g[13] = m->key_pos[k][2] + m->key_half[k][2] + 0.02f;
+    g[14] = g[15] = 0.f;
+  }
+  {
+    double y0 = m->key_ylo[0], y1 = m->key_yhi[NK - 1];
+    for (int k = 0; k < NK; k++) { y0 = fmin(y0, m->key_ylo[k]); y1 = fmax(y1, m->key_yhi[k]); }
+    double bw = (y1 - y0) / NKB;
+    m->kb_y0 = (float)y0;
+    m->kb_inv = (float)(1.0 / bw);
+    for (int b = 0; b < NKB; b++) {
+      double blo = y0 + b * bw, bhi = blo + bw;
+      int f = 0;
+      while (f < NK && m->key_yhi[f] < blo) f++;
+      int e = f;
+      while (e < NK && m->key_ylo[e] <= bhi) e++;
+      m->kb_first[b] = (uint8_t)f;
+      m->kb_end[b] = (uint8_t)e;
+    }
+  }
   for (int h = 0; h < NH; h++)
     for (int s = 0; s < PS_NFINGER; s++) {
       m->site_body[h * PS_NFINGER + s] = h * NB + d->site_body[h][s];
@@ -299,6 +325,13 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     if (m->pair[i][0] < 0 || m->pair[i][0] >= NGT || m->pair[i][1] < 0 || m->pair[i][1] >= NGT)
       return fail("capsule pair index out of range");
   }
+  // the cross-hand pairs can be skipped wholesale when the hands' boxes are apart, if they
+  // all come after the same-hand ones (model.capsule_pairs orders them so)
+  m->npairs_same = 0;
+  while (m->npairs_same < m->npairs && m->pair[m->npairs_same][0] / NG == m->pair[m->npairs_same][1] / NG)
+    m->npairs_same++;
+  for (int i = m->npairs_same; i < m->npairs; i++)
+    if (m->pair[i][0] / NG == m->pair[i][1] / NG) { m->npairs_same = m->npairs; break; }
   return 0;
 }
 

@@ -69,6 +69,22 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false));  // row_bcast:31
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
+// 64-lane min via DPP (same pattern as wave_sum; bound_ctrl off keeps the lane's own value)
+__device__ __forceinline__ float wave_min(float v) {
+  int x = __float_as_int(v);
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x111, 0xF, 0xF, false)));
+  x = __float_as_int(v);
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x112, 0xF, 0xF, false)));
+  x = __float_as_int(v);
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x114, 0xF, 0xF, false)));
+  x = __float_as_int(v);
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x118, 0xF, 0xF, false)));
+  x = __float_as_int(v);
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x142, 0xA, 0xF, false)));
+  x = __float_as_int(v);
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x143, 0xC, 0xF, false)));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ int wave_sum_i(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
@@ -90,6 +106,19 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
 }
 __device__ __forceinline__ int lanes_below(uint64_t mask, int lane) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+// exclusive prefix sum and total of small non-negative counts (< 32) by bit-plane ballots:
+// 5 ballots + mbcnt, no cross-lane data movement
+__device__ __forceinline__ int small_excl_scan(int v, int lane, int* total) {
+  int ex = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < 5; b++) {
+    const uint64_t m = __ballot((v >> b) & 1);
+    ex += lanes_below(m, lane) << b;
+    tot += __popcll(m) << b;
+  }
+  *total = tot;
+  return ex;
 }
 
 struct Contact {
@@ -141,26 +170,46 @@ __device__ float sphere_box(f3 p, float r, f3 c, const float* R, const float* hs
   return dist;
 }
 
-__device__ float seg_box_t(f3 a3, f3 d3, const float* hs) {
-  float a[3] = {a3.x, a3.y, a3.z}, dv[3] = {d3.x, d3.y, d3.z};
+// Segment parameter t in [0,1] closest to a box (box frame, half sizes hs): the squared
+// distance is convex and piecewise quadratic in t with breakpoints where the segment crosses
+// a face plane; minimise each piece in closed form. Register-only: the 8 breakpoints (0, 1
+// and the 6 plane crossings, 1 when outside (0,1)) go through a fixed sorting network.
+__device__ __forceinline__ void cswap(float& x, float& y) {
+  const float lo = fminf(x, y), hi = fmaxf(x, y);
+  x = lo;
+  y = hi;
+}
+__device__ __forceinline__ float seg_box_t(f3 a3, f3 d3, const float* hs) {
+  const float a[3] = {a3.x, a3.y, a3.z}, dv[3] = {d3.x, d3.y, d3.z};
   float bp[8];
-  int nb = 0;
-  bp[nb++] = 0.f;
+  bp[0] = 0.f;
+  bp[7] = 1.f;
+#pragma unroll
   for (int i = 0; i < 3; i++) {
-    if (dv[i] == 0.f) continue;
-    for (int sgn = -1; sgn <= 1; sgn += 2) {
-      float t = (sgn * hs[i] - a[i]) / dv[i];
-      if (t > 0.f && t < 1.f) bp[nb++] = t;
+#pragma unroll
+    for (int sg = 0; sg < 2; sg++) {
+      float t = 1.f;
+      if (dv[i] != 0.f) {
+        const float tt = ((sg ? hs[i] : -hs[i]) - a[i]) / dv[i];
+        if (tt > 0.f && tt < 1.f) t = tt;
+      }
+      bp[1 + 2 * i + sg] = t;
     }
   }
-  bp[nb++] = 1.f;
-  for (int i = 1; i < nb; i++)
-    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { float t = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = t; }
+  // Batcher odd-even merge sort network for 8 keys (19 compare-exchanges)
+  cswap(bp[0], bp[1]); cswap(bp[2], bp[3]); cswap(bp[4], bp[5]); cswap(bp[6], bp[7]);
+  cswap(bp[0], bp[2]); cswap(bp[1], bp[3]); cswap(bp[4], bp[6]); cswap(bp[5], bp[7]);
+  cswap(bp[1], bp[2]); cswap(bp[5], bp[6]);
+  cswap(bp[0], bp[4]); cswap(bp[1], bp[5]); cswap(bp[2], bp[6]); cswap(bp[3], bp[7]);
+  cswap(bp[2], bp[4]); cswap(bp[3], bp[5]);
+  cswap(bp[1], bp[2]); cswap(bp[3], bp[4]); cswap(bp[5], bp[6]);
   float bestf = INFINITY, bestt = 0.f;
-  for (int s = 0; s + 1 < nb; s++) {
-    float lo = bp[s], hi = bp[s + 1];
+#pragma unroll
+  for (int s = 0; s < 7; s++) {
+    const float lo = bp[s], hi = bp[s + 1];
     if (!(hi > lo)) continue;
     float mid = 0.5f * (lo + hi), num = 0.f, den = 0.f;
+#pragma unroll
     for (int i = 0; i < 3; i++) {
       float x = a[i] + mid * dv[i];
       float tgt = x > hs[i] ? hs[i] : (x < -hs[i] ? -hs[i] : 0.f);
@@ -170,6 +219,7 @@ __device__ float seg_box_t(f3 a3, f3 d3, const float* hs) {
     }
     float t = den > 0.f ? clampf(num / den, lo, hi) : lo;
     float f = 0.f;
+#pragma unroll
     for (int i = 0; i < 3; i++) {
       float e = fabsf(a[i] + t * dv[i]) - hs[i];
       if (e > 0) f += e * e;
