@@ -22,7 +22,7 @@ L.ps_debug_timing(g._h, out.ctypes.data)
 names = {0: "kinematics", 1: "dynamics", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
          3: "factor", 4: "solve_smooth",
          12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T", 15: "cons:finish",
-         8: "pgs", 6: "integrate"}
+         8: "pgs", 6: "integrate", 5: "final+task"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
 for i, n in names.items():
     v = out[:, i].astype(np.float64)
