@@ -134,8 +134,9 @@ def main():
     actions = [torch.rand(N, 45, device=dev, generator=gen) * 2 - 1 for _ in range(pool)]
     env.reset()
     returns = sharding.EpisodeReturns(N, dev)
-    for i in range(args.warmup):
-        env.step(actions[i % pool])
+    for i in range(args.warmup):  # also warms up the (lazily loaded) torch kernels of the return log
+        _, rew, _, st = env.step(actions[i % pool])
+        returns.update(rew, st)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
