@@ -9,6 +9,7 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("PIANOSIM_LIB", HERE / "libpianosim.so"))
+RL_LIB_PATH = Path(os.environ.get("PIANORL_LIB", HERE / "libpianorl.so"))
 
 # Every entry point declared in include/pianosim.h.
 EXPORTS = (
@@ -17,7 +18,11 @@ EXPORTS = (
     "ps_fingertips", "ps_contact_count",
 )
 
+# Every entry point declared in include/pianorl.h.
+RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample")
+
 _lib = None
+_rl = None
 
 
 class PianosimError(RuntimeError):
@@ -59,3 +64,31 @@ def check(rc: int) -> None:
     if rc != 0:
         msg = load().ps_last_error()
         raise PianosimError(msg.decode() if msg else f"pianosim error {rc}")
+
+
+def load_rl() -> C.CDLL:
+    """libpianorl.so: the on-device PPO kernels (include/pianorl.h)."""
+    global _rl
+    if _rl is not None:
+        return _rl
+    if not RL_LIB_PATH.exists():
+        raise PianosimError(
+            f"{RL_LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(RL_LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    vp, i32, u64, f32 = C.c_void_p, C.c_int, C.c_uint64, C.c_float
+    L.prl_last_error.restype = C.c_char_p
+    L.prl_version.restype = i32
+    L.prl_running_norm.argtypes = [vp, i32, vp, vp, vp]
+    L.prl_gae.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, i32, vp]
+    L.prl_normalize.argtypes = [vp, i32, f32, vp]
+    L.prl_gauss_sample.argtypes = [vp, vp, i32, i32, u64, u64, vp, vp, vp]
+    for name in RL_EXPORTS[2:]:
+        getattr(L, name).restype = i32
+    _rl = L
+    return L
+
+
+def check_rl(rc: int) -> None:
+    if rc != 0:
+        msg = load_rl().prl_last_error()
+        raise PianosimError(msg.decode() if msg else f"pianorl error {rc}")

@@ -1,0 +1,265 @@
+// pianorl.hip - MI355X (gfx950) kernels of the on-device PPO loop + the C-ABI of
+// include/pianorl.h. The reference computes these on the host (numpy RunningMeanStd,
+// a Python GAE loop, torch.distributions sampling behind a host round trip,
+// ppo_v2.py:107-131, 211-256); here they run on the rollout tensors where they live.
+//
+// All of them are HBM/latency-bound reductions and scans over a few MB at most; none is
+// GEMM-shaped, so there is no MFMA here: the layout rules are coalesced column access
+// (time-major [T, E] arrays, one thread per env column) and single-pass fp64 reductions.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/pianorl.h"
+
+namespace {
+
+thread_local std::string g_err;
+int fail(const std::string& s) {
+  g_err = s;
+  return -1;
+}
+#define HIPCHK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int RED_THREADS = 1024;
+
+// ---------------------------------------------------------------- block reductions (fp64)
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;  // valid in lane 0
+}
+
+// sum over the block; every thread gets the result
+__device__ double block_sum_d(double v, double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();  // red[] reuse across calls
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < nw; i++) s += red[i];  // fixed order: deterministic
+  return s;
+}
+
+// mean and sum of squared deviations (two passes over x, fp64 accumulation)
+__device__ void mean_m2(const float* __restrict__ x, int n, double* red, double* mean, double* m2) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += (double)x[i];
+  const double mu = block_sum_d(s, red) / (double)n;
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double d = (double)x[i] - mu;
+    q += d * d;
+  }
+  *mean = mu;
+  *m2 = block_sum_d(q, red);
+}
+
+// RunningMeanStd.__call__ (ppo_v2.py:113-131): batch statistics (np.mean / np.var, ddof 0),
+// merge into the running statistics, normalise with the merged ones.
+__global__ void __launch_bounds__(RED_THREADS) running_norm_kernel(const float* __restrict__ x, int n,
+                                                                   double* __restrict__ stats, float* __restrict__ out) {
+  __shared__ double red[RED_THREADS / 64];
+  __shared__ double nm[2];
+  double bm, bm2;
+  mean_m2(x, n, red, &bm, &bm2);
+  if (threadIdx.x == 0) {
+    const double mean = stats[0], var = stats[1], count = stats[2];
+    const double bvar = bm2 / (double)n, bc = (double)n;
+    const double delta = bm - mean, tot = count + bc;
+    const double new_mean = mean + delta * bc / tot;
+    const double M2 = var * count + bvar * bc + delta * delta * count * bc / tot;
+    const double new_var = M2 / tot;
+    stats[0] = new_mean;
+    stats[1] = new_var;
+    stats[2] = tot;
+    nm[0] = new_mean;
+    nm[1] = 1.0 / sqrt(new_var + 1e-8);
+  }
+  __syncthreads();
+  const double mu = nm[0], is = nm[1];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = (float)(((double)x[i] - mu) * is);
+}
+
+// advantages = (a - mean) / (std + eps), torch.std's unbiased estimator (ppo_v2.py:256)
+__global__ void __launch_bounds__(RED_THREADS) normalize_kernel(float* __restrict__ x, int n, float eps) {
+  __shared__ double red[RED_THREADS / 64];
+  double mu, m2;
+  mean_m2(x, n, red, &mu, &m2);
+  const double sd = n > 1 ? sqrt(m2 / (double)(n - 1)) : NAN;  // torch: nan for one sample
+  const float muf = (float)mu, den = (float)(sd + (double)eps);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) x[i] = (x[i] - muf) / den;
+}
+
+// ---------------------------------------------------------------- GAE (ppo_v2.py:234-253)
+struct GaeIn {
+  const float *r, *v, *nv, *d;
+  float *adv, *ret;
+  int T, E;
+  float gamma, gl;
+  int mode;
+};
+
+__device__ __forceinline__ float next_value(const GaeIn& g, int t, int e) {
+  return t == g.T - 1 ? g.nv[(size_t)t * g.E + e] : g.v[(size_t)(t + 1) * g.E + e];
+}
+
+__device__ __forceinline__ void gae_emit(const GaeIn& g, int t, int e, float gae) {
+  const size_t i = (size_t)t * g.E + e;
+  g.adv[i] = gae;
+  g.ret[i] = g.mode == PRL_RETURNS_TD ? g.r[i] + g.gamma * (g.nv[i] * (1.f - g.d[i])) : gae + g.v[i];
+}
+
+// many columns: one thread per env column, serial over time; row t of a warp is one
+// coalesced 256-B read per array
+__global__ void __launch_bounds__(256) gae_columns_kernel(GaeIn g) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.E) return;
+  float gae = 0.f;
+  for (int t = g.T - 1; t >= 0; t--) {
+    const size_t i = (size_t)t * g.E + e;
+    const float nd = 1.f - g.d[i];
+    const float delta = g.r[i] + g.gamma * next_value(g, t, e) * nd - g.v[i];
+    gae = delta + g.gl * nd * gae;
+    gae_emit(g, t, e, gae);
+  }
+}
+
+// few columns, long time axis (the reference's E = 1, T = batch): one block per column, the
+// linear recurrence gae_t = delta_t + c_t gae_{t+1} as a chunked scan of affine maps.
+constexpr int SCAN_THREADS = 256;
+__global__ void __launch_bounds__(SCAN_THREADS) gae_scan_kernel(GaeIn g) {
+  __shared__ float sA[SCAN_THREADS], sB[SCAN_THREADS];
+  const int e = blockIdx.x, j = threadIdx.x;
+  const int chunk = (g.T + SCAN_THREADS - 1) / SCAN_THREADS;
+  const int t0 = min(j * chunk, g.T), t1 = min(t0 + chunk, g.T);
+  // this chunk as a map g_in (gae at t1) -> gae at t0: A g_in + B
+  float A = 1.f, B = 0.f;
+  for (int t = t1 - 1; t >= t0; t--) {
+    const size_t i = (size_t)t * g.E + e;
+    const float nd = 1.f - g.d[i];
+    const float delta = g.r[i] + g.gamma * next_value(g, t, e) * nd - g.v[i];
+    const float c = g.gl * nd;
+    B = delta + c * B;
+    A = c * A;
+  }
+  sA[j] = A;
+  sB[j] = B;
+  __syncthreads();
+  // suffix composition: (A_j, B_j) <- map_j o map_{j+off}
+  for (int off = 1; off < SCAN_THREADS; off <<= 1) {
+    float a2 = 1.f, b2 = 0.f;
+    const bool has = j + off < SCAN_THREADS;
+    if (has) { a2 = sA[j + off]; b2 = sB[j + off]; }
+    __syncthreads();
+    if (has) {
+      const float a1 = sA[j], b1 = sB[j];
+      sA[j] = a1 * a2;
+      sB[j] = a1 * b2 + b1;
+    }
+    __syncthreads();
+  }
+  float gae = j + 1 < SCAN_THREADS ? sB[j + 1] : 0.f;  // gae at t1 (0 past the end)
+  for (int t = t1 - 1; t >= t0; t--) {
+    const size_t i = (size_t)t * g.E + e;
+    const float nd = 1.f - g.d[i];
+    const float delta = g.r[i] + g.gamma * next_value(g, t, e) * nd - g.v[i];
+    gae = delta + g.gl * nd * gae;
+    gae_emit(g, t, e, gae);
+  }
+}
+
+// ---------------------------------------------------------------- Gaussian policy sampling
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// one row per wave, lane = action dimension (a <= 64)
+__global__ void __launch_bounds__(256) gauss_sample_kernel(const float* __restrict__ mean, const float* __restrict__ log_std,
+                                                           int n, int a, uint64_t seed, uint64_t offset,
+                                                           float* __restrict__ action, float* __restrict__ logp) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= n) return;  // whole waves exit together
+  float lp = 0.f;
+  if (lane < a) {
+    uint32_t c[4] = {(uint32_t)lane, (uint32_t)row, (uint32_t)offset, (uint32_t)(offset >> 32)};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float u1 = ((float)c[0] + 1.f) * 2.3283064e-10f;  // (0, 1]
+    const float u2 = (float)c[1] * 2.3283064e-10f;
+    const float z = sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2);
+    const float ls = fminf(fmaxf(log_std[lane], -20.f), 2.f);
+    const float sd = expf(ls), mu = mean[(size_t)row * a + lane];
+    const float x = mu + sd * z;
+    action[(size_t)row * a + lane] = x;
+    // torch.distributions.Normal.log_prob: -((x - mu)^2) / (2 var) - log(scale) - log(sqrt(2 pi))
+    const float dx = x - mu;
+    lp = -(dx * dx) / (2.f * sd * sd) - logf(sd) - 0.91893853f;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lp += __shfl_down(lp, off, 64);
+  if (lane == 0) logp[row] = lp;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C-ABI
+extern "C" {
+
+const char* prl_last_error(void) { return g_err.c_str(); }
+int prl_version(void) { return 1; }
+
+int prl_running_norm(const float* x, int n, double* stats, float* out, void* stream) {
+  if (!x || !stats || !out || n <= 0) return fail("prl_running_norm: null pointer or n <= 0");
+  running_norm_kernel<<<1, RED_THREADS, 0, (hipStream_t)stream>>>(x, n, stats, out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_gae(const float* rewards, const float* values, const float* next_values, const float* dones, float* adv,
+            float* ret, int T, int E, float gamma, float lam, int returns_mode, void* stream) {
+  if (!rewards || !values || !next_values || !dones || !adv || !ret) return fail("prl_gae: null pointer");
+  if (T <= 0 || E <= 0) return fail("prl_gae: T and E must be positive");
+  if (returns_mode != PRL_RETURNS_TD && returns_mode != PRL_RETURNS_GAE) return fail("prl_gae: bad returns_mode");
+  GaeIn g{rewards, values, next_values, dones, adv, ret, T, E, gamma, gamma * lam, returns_mode};
+  if (E >= 256 || T <= 64)
+    gae_columns_kernel<<<(E + 255) / 256, 256, 0, (hipStream_t)stream>>>(g);
+  else
+    gae_scan_kernel<<<E, SCAN_THREADS, 0, (hipStream_t)stream>>>(g);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_normalize(float* x, int n, float eps, void* stream) {
+  if (!x || n <= 0) return fail("prl_normalize: null pointer or n <= 0");
+  normalize_kernel<<<1, RED_THREADS, 0, (hipStream_t)stream>>>(x, n, eps);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint64_t seed, uint64_t offset,
+                     float* action, float* logp, void* stream) {
+  if (!mean || !log_std || !action || !logp) return fail("prl_gauss_sample: null pointer");
+  if (n <= 0 || a <= 0 || a > 64) return fail("prl_gauss_sample: need n > 0 and 0 < a <= 64");
+  gauss_sample_kernel<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(mean, log_std, n, a, seed, offset, action, logp);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

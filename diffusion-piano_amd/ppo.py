@@ -1,0 +1,549 @@
+"""On-device PPO agent: the consumer of the hot path.
+
+Mirrors ``ppo_v2.py`` (AlmondGod/diffusion-piano) so the reference driver
+(``parallelized_base_v2.py:70-189``) runs against it unchanged - same class and method
+names, constructor arguments, network layouts (``state_dict`` keys load both ways),
+optimiser / scheduler settings, update math and checkpoint format - while every tensor of
+the loop stays in HBM:
+
+* :class:`Actor` / :class:`Critic` - ``ppo_v2.py:51-105`` (torch modules; the GEMMs run on
+  hipBLASLt).
+* :class:`RunningMeanStd` - ``ppo_v2.py:107-131``; statistics live on the device and are
+  merged by ``prl_running_norm`` (libpianorl.so) in fp64, as the reference's numpy.
+* :class:`PPOAgent` - ``ppo_v2.py:133-336``. ``select_actions`` samples with the fused
+  ``prl_gauss_sample`` kernel; ``update`` runs the reward normaliser, the GAE scan
+  (``prl_gae``) and the advantage normalisation (``prl_normalize``) on the device, then the
+  10 epochs of shuffled minibatches with the minibatch step captured once in a HIP graph
+  and replayed (the reference launches ~150 kernels and 6 host syncs per minibatch).
+
+Semantics kept from the reference, on purpose:
+
+* ``update(states[N], ...)`` runs the GAE recursion over the BATCH axis, exactly as
+  ``ppo_v2.py:245-253`` does (a reference bug); the returns are the
+  TD targets ``r + gamma V(s') (1 - d)`` (``:234-237``). Passing time-major rollouts
+  ``[T, E, ...]`` instead runs the proper time-axis GAE with ``adv + V`` returns
+  (:class:`RolloutTrainer`).
+* The minibatch order is the one ``DataLoader(shuffle=True)`` draws: per epoch two draws
+  of the global CPU generator (the loader's base seed, then the sampler's seed) and
+  ``randperm`` on a CPU generator seeded with the second (verified against torch's own
+  DataLoader in tests/test_ppo.py).
+* The critic stays in train mode (its Dropout is active in ``update``, as in the
+  reference); the actor loss and the critic loss are independent, so both backward passes
+  run before both optimiser steps (same result as the reference's critic-then-actor order).
+
+Data parallel: with ``process_group`` set, the gradients of both
+networks live in one flat bucket that is all-reduced (RCCL over xGMI) once per minibatch,
+between the captured backward graph and the captured optimiser graph.
+
+There is no CPU fallback: the agent needs a ROCm GPU and libpianorl.so.
+"""
+
+from __future__ import annotations
+
+import math
+import time
+import warnings
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.distributions import Normal
+
+from . import _lib, abi
+
+_LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
+LOG_KEYS = ("actor_loss", "critic_loss", "entropy", "value_predictions", "returns", "advantages")
+
+
+# ---------------------------------------------------------------- networks (ppo_v2.py:51-105)
+class Actor(nn.Module):
+    def __init__(self, state_dim, action_dim, hidden_dim=256):
+        super().__init__()
+        self.network = nn.Sequential(
+            nn.Linear(state_dim, hidden_dim), nn.ReLU(), nn.LayerNorm(hidden_dim),
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.LayerNorm(hidden_dim),
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.LayerNorm(hidden_dim),
+            nn.Linear(hidden_dim, action_dim), nn.Tanh(),
+        )
+        self.log_std = nn.Parameter(torch.ones(action_dim) * -1.0)
+
+    def forward(self, state):
+        mean = self.network(state)
+        std = torch.exp(torch.clamp(self.log_std, -20, 2))
+        return Normal(mean, std)
+
+
+class Critic(nn.Module):
+    def __init__(self, state_dim, hidden_dim=256):
+        super().__init__()
+        self.network = nn.Sequential(
+            nn.Linear(state_dim, hidden_dim), nn.ReLU(), nn.LayerNorm(hidden_dim), nn.Dropout(0.1),
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.LayerNorm(hidden_dim), nn.Dropout(0.1),
+            nn.Linear(hidden_dim, hidden_dim // 2), nn.ReLU(), nn.LayerNorm(hidden_dim // 2),
+            nn.Linear(hidden_dim // 2, 1),
+        )
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.orthogonal_(m.weight, gain=0.01)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    def forward(self, state):
+        return self.network(state)
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _f32(x, device):
+    return torch.as_tensor(x, device=device, dtype=torch.float32).contiguous()
+
+
+# ---------------------------------------------------------------- kernels (include/pianorl.h)
+def gae(rewards, values, next_values, dones, gamma=0.99, lam=0.95, returns_mode=0):
+    """Time-major ``[T, E]`` (or ``[T]``) device tensors -> (advantages, returns). ``prl_gae``."""
+    r = rewards.contiguous()
+    T = r.shape[0]
+    E = r.numel() // T
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    _lib.check_rl(_lib.load_rl().prl_gae(r.data_ptr(), values.contiguous().data_ptr(), next_values.contiguous().data_ptr(),
+                                         dones.contiguous().data_ptr(), adv.data_ptr(), ret.data_ptr(), T, E,
+                                         float(gamma), float(lam), int(returns_mode), _stream()))
+    return adv, ret
+
+
+def normalize_(x, eps=1e-8):
+    """In place ``(x - mean) / (std + eps)`` (unbiased std). ``prl_normalize``."""
+    assert x.is_contiguous() and x.dtype == torch.float32
+    _lib.check_rl(_lib.load_rl().prl_normalize(x.data_ptr(), x.numel(), float(eps), _stream()))
+    return x
+
+
+def gauss_sample(mean, log_std, seed, offset):
+    """-> (actions [N, A], log_prob sums [N]). ``prl_gauss_sample``."""
+    mean = mean.contiguous()
+    n, a = mean.shape
+    act = torch.empty_like(mean)
+    lp = torch.empty(n, device=mean.device, dtype=torch.float32)
+    _lib.check_rl(_lib.load_rl().prl_gauss_sample(mean.data_ptr(), log_std.detach().contiguous().data_ptr(), n, a,
+                                                  int(seed) & (2**64 - 1), int(offset), act.data_ptr(), lp.data_ptr(),
+                                                  _stream()))
+    return act, lp
+
+
+# ---------------------------------------------------------------- RunningMeanStd (ppo_v2.py:107-131)
+class RunningMeanStd:
+    """Scalar running statistics in HBM (``shape=()``, the only one the agent uses)."""
+
+    def __init__(self, epsilon=1e-4, shape=(), device=None):
+        if tuple(shape) != ():
+            raise ValueError("RunningMeanStd: only shape=() is implemented (what PPOAgent uses)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.stats = torch.tensor([0.0, 1.0, epsilon], dtype=torch.float64, device=self.device)
+
+    # host views (synchronising; for inspection and checkpoints)
+    @property
+    def mean(self):
+        return float(self.stats[0])
+
+    @property
+    def var(self):
+        return float(self.stats[1])
+
+    @property
+    def count(self):
+        return float(self.stats[2])
+
+    def normalize_(self, x):
+        """Device tensor -> fp32 device tensor normalised with the merged statistics."""
+        x = _f32(x, self.device).reshape(-1)
+        out = torch.empty_like(x)
+        _lib.check_rl(_lib.load_rl().prl_running_norm(x.data_ptr(), x.numel(), self.stats.data_ptr(), out.data_ptr(),
+                                                      _stream()))
+        return out
+
+    def __call__(self, x):
+        if isinstance(x, torch.Tensor):
+            return self.normalize_(x).reshape(x.shape)
+        arr = np.asarray(x, np.float64)
+        return self.normalize_(torch.from_numpy(arr.astype(np.float32))).cpu().numpy().astype(np.float64).reshape(arr.shape)
+
+
+class RolloutBuffer:
+    """``ppo_v2.py:13-49`` (kept for API parity; the drivers do not use it)."""
+
+    def __init__(self, batch_size=64):
+        self.batch_size = batch_size
+        self.clear()
+
+    def push(self, state, action, reward, log_prob, next_state, done):
+        for k, v in zip(("states", "actions", "rewards", "log_probs", "next_states", "dones"),
+                        (state, action, reward, log_prob, next_state, done)):
+            getattr(self, k).append(v)
+
+    def get(self):
+        return tuple(torch.FloatTensor(np.array(getattr(self, k))) for k in
+                     ("states", "actions", "rewards", "log_probs", "next_states", "dones"))
+
+    def clear(self):
+        self.states, self.actions, self.rewards = [], [], []
+        self.log_probs, self.next_states, self.dones = [], [], []
+
+
+# ---------------------------------------------------------------- DataLoader order
+def loader_permutation(n: int) -> torch.Tensor:
+    """The index order ``DataLoader(dataset, shuffle=True)`` yields for one epoch: the
+    iterator draws its base seed, then ``RandomSampler`` draws a seed for a fresh CPU
+    generator and returns ``randperm`` from it (torch/utils/data/{dataloader,sampler}.py)."""
+    torch.empty((), dtype=torch.int64).random_()
+    seed = int(torch.empty((), dtype=torch.int64).random_().item())
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g)
+
+
+# ---------------------------------------------------------------- gradient bucket (DP)
+class GradBucket:
+    """One flat fp32 buffer holding the gradients of ``params`` (``p.grad`` are views), so
+    data-parallel training does one all-reduce per minibatch instead of one per tensor."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=self.params[0].device)
+        o = 0
+        for p in self.params:
+            p.grad = self.flat[o:o + p.numel()].view_as(p)
+            o += p.numel()
+
+    def allreduce_(self, group=None):
+        import torch.distributed as dist
+        ws = dist.get_world_size(group)
+        if ws > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            self.flat.div_(ws)
+
+
+# ---------------------------------------------------------------- the agent (ppo_v2.py:133-336)
+class PPOAgent:
+    def __init__(self, state_dim, action_dim, lr=1e-4, gamma=0.99, epsilon=0.2, entropy_coef=0.01, value_coef=1.0,
+                 max_grad_norm=0.5, ppo_epochs=10, batch_size=64, device="cuda", checkpoint_dir="checkpoints",
+                 use_wandb=True, *, gae_lambda=0.95, process_group=None, graphs=True, sample_seed=None):
+        if not torch.cuda.is_available():
+            raise _lib.PianosimError("PPOAgent needs a ROCm GPU (torch.cuda.is_available() is False)")
+        _lib.load_rl()  # fail loudly if the kernels are missing
+        self.device = torch.device(device if str(device).startswith("cuda") else "cuda")
+        self.actor = Actor(state_dim, action_dim).to(self.device)
+        self.critic = Critic(state_dim).to(self.device)
+        self.process_group = process_group
+        self.distributed = process_group is not None or (
+            torch.distributed.is_available() and torch.distributed.is_initialized()
+            and torch.distributed.get_world_size() > 1)
+        if self.distributed:  # identical replicas: rank 0's initial weights everywhere
+            for p in list(self.actor.parameters()) + list(self.critic.parameters()):
+                torch.distributed.broadcast(p.data, src=0, group=process_group)
+        self.bucket = GradBucket(list(self.critic.parameters()) + list(self.actor.parameters()))
+        adam = dict(betas=(0.9, 0.999), eps=1e-5, capturable=True, foreach=True)
+        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(),
+                                                lr=torch.tensor(float(lr), device=self.device), **adam)
+        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(),
+                                                 lr=torch.tensor(float(lr) * 2, device=self.device), **adam)
+        self.actor_scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.actor_optimizer, mode="max", factor=0.5,
+                                                                          patience=100)
+        self.critic_scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.critic_optimizer, mode="min",
+                                                                           factor=0.5, patience=100)
+        self.reward_normalizer = RunningMeanStd(device=self.device)
+        self.max_grad_norm = max_grad_norm
+        self.gamma = gamma
+        self.gae_lambda = gae_lambda
+        self.epsilon = epsilon
+        self.entropy_coef = entropy_coef
+        self.value_coef = value_coef  # stored, unused in the loss: as the reference (ppo_v2.py:287)
+        self.ppo_epochs = ppo_epochs
+        self.batch_size = batch_size
+        self.rollout_buffer = RolloutBuffer(batch_size)
+        self.checkpoint_dir = Path(checkpoint_dir)
+        self.checkpoint_dir.mkdir(parents=True, exist_ok=True)
+        self.use_wandb = use_wandb
+        self._wandb = None
+        if use_wandb:
+            try:
+                import wandb
+                self._wandb = wandb
+                wandb.init(project="robopianist-ppo", config=dict(lr=lr, gamma=gamma, epsilon=epsilon,
+                                                                   entropy_coef=entropy_coef, value_coef=value_coef,
+                                                                   ppo_epochs=ppo_epochs, batch_size=batch_size))
+            except ImportError:
+                warnings.warn("wandb is not installed: PPOAgent logs stay in agent.last_update_log")
+        self.graphs = graphs
+        self._seed = (torch.initial_seed() if sample_seed is None else int(sample_seed)) ^ 0x5DEECE66D
+        self._offset = 0
+        self._cap = 0
+        self._graph = None
+        self._graph_eager_left = 2
+        self._cap_stream = torch.cuda.Stream(self.device)
+        self.last_update_log = None
+        self.timing = {}
+
+    # -- acting (ppo_v2.py:211-218)
+    def select_actions(self, states):
+        as_numpy = not isinstance(states, torch.Tensor)
+        s = _f32(states, self.device)
+        with torch.no_grad():
+            mean = self.actor.network(s)
+        actions, log_probs = gauss_sample(mean, self.actor.log_std, self._seed, self._offset)
+        self._offset += 1
+        if as_numpy:
+            return actions.cpu().numpy(), log_probs.cpu().numpy()
+        return actions, log_probs
+
+    # -- minibatch step (ppo_v2.py:266-293): forward + both backwards | all-reduce | clip + steps
+    def _forward_backward(self, idx, log_row):
+        b_s = self._S.index_select(0, idx)
+        b_a = self._A.index_select(0, idx)
+        b_lp = self._LP.index_select(0, idx)
+        b_adv = self._ADV.index_select(0, idx)
+        b_ret = self._RET.index_select(0, idx)
+        # Normal(mean, std).log_prob / .entropy written out with torch.distributions' own
+        # formulas: the distribution object validates its arguments with a host sync, which
+        # cannot sit inside a captured graph
+        mean = self.actor.network(b_s)
+        log_scale = torch.log(torch.exp(torch.clamp(self.actor.log_std, -20, 2)))
+        var = torch.exp(torch.clamp(self.actor.log_std, -20, 2)) ** 2
+        new_lp = (-((b_a - mean) ** 2) / (2 * var) - log_scale - _LOG_SQRT_2PI).sum(1)
+        entropy = (0.5 + 0.5 * math.log(2 * math.pi) + log_scale).expand_as(mean).mean()
+        ratio = torch.exp(new_lp - b_lp)
+        surr1 = ratio * b_adv
+        surr2 = torch.clamp(ratio, 1 - self.epsilon, 1 + self.epsilon) * b_adv
+        actor_loss = -torch.min(surr1, surr2).mean() - self.entropy_coef * entropy
+        value_pred = self.critic(b_s).squeeze(-1)
+        critic_loss = F.mse_loss(value_pred, b_ret)
+        self.critic_optimizer.zero_grad(set_to_none=False)
+        self.actor_optimizer.zero_grad(set_to_none=False)
+        critic_loss.backward()
+        actor_loss.backward()
+        log_row.copy_(torch.stack([actor_loss, critic_loss, entropy, value_pred.mean(), b_ret.mean(),
+                                   b_adv.mean()]).detach())
+
+    def _clip_step(self):
+        torch.nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad_norm, foreach=True)
+        self.critic_optimizer.step()
+        torch.nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad_norm, foreach=True)
+        self.actor_optimizer.step()
+
+    def _eager_step(self, idx, log_row):
+        self._forward_backward(idx, log_row)
+        if self.distributed:
+            self.bucket.allreduce_(self.process_group)
+        self._clip_step()
+
+    def _warmup_step(self):
+        """A real minibatch step, run eagerly on the capture stream before capturing (BLAS
+        handles / workspaces and the optimiser state then exist outside the capture)."""
+        s = self._cap_stream
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._eager_step(self._idx, self._log_row)
+        torch.cuda.current_stream().wait_stream(s)
+
+    def _capture(self):
+        """Capture the full-size minibatch step as HIP graph(s): one graph on a single GPU;
+        [forward+backward] and [clip+step] around the eager all-reduce when distributed."""
+        pool = torch.cuda.graph_pool_handle()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=pool, stream=self._cap_stream):
+            self._forward_backward(self._idx, self._log_row)
+            if not self.distributed:
+                self._clip_step()
+        g2 = None
+        if self.distributed:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool, stream=self._cap_stream):
+                self._clip_step()
+        self._graph = (g1, g2)
+
+    def _replay(self):
+        g1, g2 = self._graph
+        g1.replay()
+        if g2 is not None:
+            self.bucket.allreduce_(self.process_group)
+            g2.replay()
+
+    def _ensure_capacity(self, n, sdim, adim):
+        if n <= self._cap and self._S.shape[1] == sdim and self._A.shape[1] == adim:
+            return
+        f32 = dict(device=self.device, dtype=torch.float32)
+        self._cap = n
+        self._S = torch.empty(n, sdim, **f32)
+        self._A = torch.empty(n, adim, **f32)
+        self._LP = torch.empty(n, **f32)
+        self._ADV = torch.empty(n, **f32)
+        self._RET = torch.empty(n, **f32)
+        self._idx = torch.zeros(self.batch_size, device=self.device, dtype=torch.int64)
+        self._log_row = torch.zeros(len(LOG_KEYS), **f32)
+        self._graph = None  # buffers moved: re-capture
+        self._graph_eager_left = 2
+
+    def _prepare(self, states, actions, rewards, log_probs, next_states, dones):
+        """Reward normalisation, critic values, GAE, advantage normalisation (ppo_v2.py:221-256).
+        Returns (normalised rewards, number of samples)."""
+        dev = self.device
+        s = _f32(states, dev)
+        a = _f32(actions, dev)
+        lp = _f32(log_probs, dev).reshape(-1)
+        ns = _f32(next_states, dev)
+        d = _f32(dones, dev)
+        r = self.reward_normalizer(_f32(rewards, dev))
+        time_major = s.dim() == 3
+        with torch.no_grad():
+            if time_major:  # [T, E, D]: values of every step, bootstrap from the last next state
+                T, E = s.shape[:2]
+                values = self.critic(s.reshape(T * E, -1)).reshape(T, E)
+                next_values = self.critic(ns[-1] if ns.dim() == 3 else ns).reshape(1, E).expand(T, E).contiguous()
+                adv, ret = gae(r.reshape(T, E), values, next_values, d.reshape(T, E), self.gamma, self.gae_lambda,
+                               returns_mode=1)
+            else:  # the reference's batch-axis recursion and TD returns
+                values = self.critic(s).squeeze(-1)
+                next_values = self.critic(ns).squeeze(-1)
+                adv, ret = gae(r, values, next_values, d, self.gamma, self.gae_lambda, returns_mode=0)
+        n = adv.numel()
+        adv = normalize_(adv.reshape(-1))
+        sdim, adim = s.shape[-1], a.shape[-1]
+        self._ensure_capacity(n, sdim, adim)
+        self._S[:n].copy_(s.reshape(n, sdim))
+        self._A[:n].copy_(a.reshape(n, adim))
+        self._LP[:n].copy_(lp)
+        self._ADV[:n].copy_(adv)
+        self._RET[:n].copy_(ret.reshape(-1))
+        return r, n
+
+    # -- update (ppo_v2.py:220-309)
+    def update(self, states, actions, rewards, log_probs, next_states, dones):
+        t0 = time.perf_counter()
+        r, n = self._prepare(states, actions, rewards, log_probs, next_states, dones)
+        B = self.batch_size
+        nmb = (n + B - 1) // B
+        log = torch.empty(self.ppo_epochs * nmb, len(LOG_KEYS), device=self.device)
+        row = 0
+        for _ in range(self.ppo_epochs):
+            perm = loader_permutation(n).to(self.device, non_blocking=True)
+            for i in range(nmb):
+                idx = perm[i * B:(i + 1) * B]
+                if idx.numel() == B and self.graphs:
+                    self._idx.copy_(idx)
+                    if self._graph is None and self._graph_eager_left > 0:
+                        self._warmup_step()
+                        self._graph_eager_left -= 1
+                    else:
+                        if self._graph is None:
+                            self._capture()
+                        self._replay()
+                    log[row].copy_(self._log_row)
+                else:
+                    self._eager_step(idx, log[row])
+                row += 1
+        self.last_update_log = log
+        if self._wandb is not None:
+            for rec in log.cpu().numpy():
+                self._wandb.log(dict(zip(LOG_KEYS, map(float, rec))))
+        mean_reward = r.mean().item()
+        mean_critic_loss = float(log[-1, 1])
+        self.actor_scheduler.step(mean_reward)
+        self.critic_scheduler.step(mean_critic_loss)
+        self.timing["update_s"] = time.perf_counter() - t0
+
+    # -- checkpoints (ppo_v2.py:311-336, ppo_base.py:150-155)
+    def _state(self):
+        return {
+            "actor_state_dict": self.actor.state_dict(),
+            "critic_state_dict": self.critic.state_dict(),
+            "actor_optimizer_state_dict": self.actor_optimizer.state_dict(),
+            "critic_optimizer_state_dict": self.critic_optimizer.state_dict(),
+            "actor_scheduler_state_dict": self.actor_scheduler.state_dict(),
+            "critic_scheduler_state_dict": self.critic_scheduler.state_dict(),
+        }
+
+    def save_checkpoint(self, episode, rewards):
+        ck = dict(episode=episode, rewards=rewards, reward_normalizer=self.reward_normalizer.stats.cpu(), **self._state())
+        path = self.checkpoint_dir / f"checkpoint_episode_{episode}.pt"
+        torch.save(ck, path)
+        if self._wandb is not None:
+            self._wandb.save(str(path))
+        print(f"Saved checkpoint to {path}")
+        return path
+
+    def load_checkpoint(self, path):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.actor.load_state_dict(ck["actor_state_dict"])
+        self.critic.load_state_dict(ck["critic_state_dict"])
+        self.actor_optimizer.load_state_dict(ck["actor_optimizer_state_dict"])
+        self.critic_optimizer.load_state_dict(ck["critic_optimizer_state_dict"])
+        self.actor_scheduler.load_state_dict(ck["actor_scheduler_state_dict"])
+        self.critic_scheduler.load_state_dict(ck["critic_scheduler_state_dict"])
+        if "reward_normalizer" in ck:
+            self.reward_normalizer.stats.copy_(ck["reward_normalizer"])
+        self._graph = None  # optimiser state tensors were replaced: re-capture
+        self._graph_eager_left = 2
+
+    def save_model(self, path):
+        torch.save({"actor_state_dict": self.actor.state_dict(), "critic_state_dict": self.critic.state_dict()}, path)
+
+
+# ---------------------------------------------------------------- time-axis rollouts
+class RolloutTrainer:
+    """The MI355X-first loop: ``horizon`` control steps of all envs are collected into
+    time-major HBM buffers (observations never leave the device), then one PPO update runs
+    with time-axis GAE over ``[horizon, N]``. ``reference_semantics=True`` instead calls
+    ``agent.update`` after every env step with that step's batch, as
+    ``parallelized_base_v2.py:116-166`` does."""
+
+    def __init__(self, env, agent: PPOAgent, horizon: int = 16, reference_semantics: bool = False):
+        self.env, self.agent = env, agent
+        self.horizon = horizon
+        self.reference_semantics = reference_semantics
+        N, D = env.num_envs, env.obs_dim
+        f32 = dict(device=env.device, dtype=torch.float32)
+        H = 1 if reference_semantics else horizon
+        self.obs = torch.empty(H, N, D, **f32)
+        self.act = torch.empty(H, N, 45, **f32)
+        self.logp = torch.empty(H, N, **f32)
+        self.rew = torch.empty(H, N, **f32)
+        self.done = torch.empty(H, N, **f32)
+        self.ep_return = torch.zeros(N, **f32)
+        self.return_sum = torch.zeros((), **f32)  # over finished episodes (device; read when logging)
+        self.episodes = torch.zeros((), **f32)
+        self._cur = env.reset().clone()
+
+    def _act_step(self, t):
+        env = self.env
+        self.obs[t].copy_(self._cur)
+        a, lp = self.agent.select_actions(self._cur)
+        self.act[t].copy_(a)
+        self.logp[t].copy_(lp)
+        obs, rew, _, st = env.step(a)
+        self.rew[t].copy_(rew)
+        done = self.done[t]
+        done.copy_(st == abi.LAST)
+        self.ep_return += rew
+        self.return_sum += (self.ep_return * done).sum()
+        self.episodes += done.sum()
+        self.ep_return.mul_(1.0 - done)
+        self._cur.copy_(obs)
+
+    def iterate(self):
+        """One outer iteration; returns the number of env-steps taken."""
+        N = self.env.num_envs
+        if self.reference_semantics:
+            self._act_step(0)
+            self.agent.update(self.obs[0], self.act[0], self.rew[0], self.logp[0], self._cur, self.done[0])
+            return N
+        for t in range(self.horizon):
+            self._act_step(t)
+        nxt = self._cur.unsqueeze(0)
+        self.agent.update(self.obs, self.act, self.rew, self.logp, nxt, self.done)
+        return self.horizon * N

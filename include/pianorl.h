@@ -1,0 +1,61 @@
+/*
+ * pianorl.h - C-ABI of the on-device PPO kernels (the
+ * consumer of the hot path, ppo_v2.py's PPOAgent, moved into HBM).
+ *
+ * The reference has no FFI here either: its agent is Python over torch, with the rollout
+ * statistics computed on the host in numpy / Python loops. These entry points replace
+ * those host loops; the MLPs stay torch modules (hipBLASLt GEMMs) and are driven by
+ * diffusion-piano_amd/ppo.py, which binds this library with ctypes:
+ *
+ *   prl_running_norm  <- RunningMeanStd.__call__ (ppo_v2.py:113-131): batch mean / population
+ *                        variance, running-statistics merge (Chan et al.), normalise with the
+ *                        merged statistics. fp64 statistics, as the reference's numpy.
+ *   prl_gae           <- the GAE loop of PPOAgent.update (ppo_v2.py:239-253) and the TD
+ *                        returns (:234-237). Layout [T, E] (time-major). E = 1, T = batch
+ *                        reproduces the reference exactly (it runs the recursion over the
+ *                        env batch axis); E = envs gives the time-axis GAE of a rollout.
+ *   prl_normalize     <- advantages = (a - a.mean()) / (a.std() + 1e-8) (ppo_v2.py:256),
+ *                        unbiased std as torch.std.
+ *   prl_gauss_sample  <- select_actions: Normal(mean, exp(clamp(log_std,-20,2))).sample() and
+ *                        log_prob(actions).sum(1) (ppo_v2.py:70-74, 211-218). Counter-based
+ *                        Philox4x32-10 keyed by (seed, offset, row, column).
+ *
+ * Conventions as include/pianosim.h: DEVICE pointers, asynchronous on the caller's HIP
+ * stream (NULL = default), 0 = OK / < 0 = error with a thread-local prl_last_error().
+ */
+#ifndef PIANORL_H
+#define PIANORL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* returns_mode of prl_gae */
+#define PRL_RETURNS_TD 0  /* ret = r + gamma * next_values * (1 - done)   (ppo_v2.py:234-237) */
+#define PRL_RETURNS_GAE 1 /* ret = adv + values                           (standard PPO target) */
+
+const char* prl_last_error(void);
+int prl_version(void);
+
+/* x[n] f32 -> out[n] f32; stats[3] f64 = {mean, var, count}, updated in place. */
+int prl_running_norm(const float* x, int n, double* stats, float* out, void* stream);
+
+/* rewards/values/next_values/dones [T*E] f32 (dones 0/1) -> adv, ret [T*E] f32.
+ * delta_t = r_t + gamma * nv_t * (1 - d_t) - v_t, nv_t = values[t+1] (t < T-1) else
+ * next_values[T-1]; gae_t = delta_t + gamma * lam * (1 - d_t) * gae_{t+1}. */
+int prl_gae(const float* rewards, const float* values, const float* next_values, const float* dones,
+            float* adv, float* ret, int T, int E, float gamma, float lam, int returns_mode, void* stream);
+
+/* x[n] f32, in place: (x - mean) / (std_unbiased + eps). */
+int prl_normalize(float* x, int n, float eps, void* stream);
+
+/* mean[n, a] f32, log_std[a] f32 -> action[n, a], logp[n] (sum over a). a <= 64. */
+int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint64_t seed, uint64_t offset,
+                     float* action, float* logp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

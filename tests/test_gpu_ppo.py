@@ -1,0 +1,176 @@
+"""GPU parity of the on-device PPO path (libpianorl.so + diffusion-piano_amd/ppo.py).
+
+* prl_gae / prl_running_norm / prl_normalize / prl_gauss_sample against the CPU
+  restatement (oracle/rl_ref.py) on seeded inputs, every launch shape the wrapper picks
+  (column kernel, chunked-scan kernel, T = 1, the reference's E = 1 / T = batch case).
+  Tolerances: GAE 2e-5 relative to the largest |advantage| (fp32 scan vs fp64 loop, the
+  chunked scan reassociates the recursion), statistics 1e-12 relative (fp64 on both sides),
+  log-probs 1e-5 relative.
+* PPOAgent.update against tests/golden/ppo_v2.npz, the reference's own agent run on CPU:
+  per-minibatch losses / entropy / value / return / advantage means, the normaliser
+  statistics and sampled weights after two update() calls (first call: two eager
+  warm-up minibatches, then the HIP-graph replay; second call: all graph replays).
+  Tolerance: 2e-4 relative on the logged scalars and 5e-6 absolute on the weights (fp32 GPU
+  GEMMs vs fp32 CPU GEMMs, 12 Adam steps of lr 1e-4 / 2e-4).
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from test_ppo import golden, golden_batch, load_critic_state, sample_index  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ppo():
+    return importlib.import_module("diffusion-piano_amd.ppo")
+
+
+@pytest.fixture(scope="module")
+def rl():
+    return importlib.import_module("rl_ref")
+
+
+def dev(x):
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float32, device="cuda:0")
+
+
+@pytest.mark.parametrize("T,E", [(96, 1), (4096, 1), (1000, 3), (166, 4096), (7, 5), (1, 9), (300, 300), (257, 2)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gae_matches_restatement(ppo, rl, T, E, mode):
+    rng = np.random.RandomState(T * 31 + E)
+    r, v, nv = rng.randn(T, E), rng.randn(T, E), rng.randn(T, E)
+    d = (rng.rand(T, E) < 0.05).astype(np.float64)
+    adv, ret = ppo.gae(dev(r), dev(v), dev(nv), dev(d), 0.99, 0.95, returns_mode=mode)
+    a_ref, r_ref = rl.gae(r.astype(np.float32), v.astype(np.float32), nv.astype(np.float32), d, 0.99, 0.95, mode)
+    scale = max(1.0, np.abs(a_ref).max())
+    np.testing.assert_allclose(adv.cpu().numpy(), a_ref, atol=2e-5 * scale, rtol=0)
+    np.testing.assert_allclose(ret.cpu().numpy(), r_ref, atol=2e-5 * scale, rtol=0)
+
+
+@pytest.mark.parametrize("n", [1, 96, 4096, 680000])
+def test_running_norm_and_normalize(ppo, rl, n):
+    rng = np.random.RandomState(n)
+    rms = ppo.RunningMeanStd(device="cuda:0")
+    stats = (0.0, 1.0, 1e-4)
+    for k in range(3):
+        x = (rng.randn(n) * (k + 1) + k).astype(np.float32)
+        out = rms(dev(x))
+        stats, want = rl.running_norm(stats, x)
+        np.testing.assert_allclose(rms.stats.cpu().numpy(), stats, rtol=1e-12)
+        np.testing.assert_allclose(out.cpu().numpy(), want, rtol=1e-5, atol=1e-6)
+    if n > 1:
+        x = (rng.randn(n) * 3 + 1).astype(np.float32)
+        y = ppo.normalize_(dev(x))
+        np.testing.assert_allclose(y.cpu().numpy(), rl.normalize(x), rtol=1e-5, atol=1e-5)
+
+
+def test_gauss_sample(ppo, rl):
+    n, a = 20000, 45
+    rng = np.random.RandomState(5)
+    mean = dev(rng.uniform(-1, 1, (n, a)))
+    log_std = dev(np.linspace(-2.0, 0.5, a))
+    act, lp = ppo.gauss_sample(mean, log_std, seed=1234, offset=7)
+    act2, lp2 = ppo.gauss_sample(mean, log_std, seed=1234, offset=7)
+    act3, _ = ppo.gauss_sample(mean, log_std, seed=1234, offset=8)
+    assert torch.equal(act, act2) and torch.equal(lp, lp2)  # counter-based: reproducible
+    assert not torch.equal(act, act3)
+    want = rl.gauss_logp(mean.cpu().numpy(), log_std.cpu().numpy(), act.cpu().numpy())
+    np.testing.assert_allclose(lp.cpu().numpy(), want, rtol=1e-5, atol=1e-4)
+    z = ((act - mean) / torch.exp(log_std)).cpu().numpy().astype(np.float64)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    assert abs(np.corrcoef(z[:, 0], z[:, 1])[0, 1]) < 0.03  # lanes are independent streams
+    # torch's Normal.log_prob on the same actions
+    d = torch.distributions.Normal(mean, torch.exp(torch.clamp(log_std, -20, 2)))
+    torch.testing.assert_close(lp, d.log_prob(act).sum(1), rtol=1e-5, atol=1e-4)
+
+
+def _agent(ppo, z, tmp_path, graphs=True):
+    torch.manual_seed(int(z["meta"][5]))
+    S, A, N, B, EP = (int(x) for x in z["meta"][:5])
+    agent = ppo.PPOAgent(S, A, lr=1e-4, gamma=0.99, epsilon=0.2, batch_size=B, ppo_epochs=EP, device="cuda",
+                         checkpoint_dir=str(tmp_path), use_wandb=False, graphs=graphs)
+    agent.critic.eval()  # dropout off, as the golden run (make_ppo_golden.py)
+    load_critic_state(agent.critic)  # the golden run's portable critic start state
+    return agent
+
+
+def _params(agent):
+    p = {"actor." + k: v for k, v in agent.actor.state_dict().items()}
+    p.update({"critic." + k: v for k, v in agent.critic.state_dict().items()})
+    return p
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_update_matches_reference_agent(ppo, tmp_path, graphs):
+    z = golden()
+    agent = _agent(ppo, z, tmp_path, graphs)
+    for k, v in _params(agent).items():
+        if k.startswith("actor."):
+            flat = v.reshape(-1).cpu().numpy()
+            np.testing.assert_array_equal(flat[sample_index(flat.size)], z["init/" + k], err_msg=k)
+    for call, seed in enumerate(int(x) for x in z["meta"][6:8]):
+        s, a, r, lp, ns, d = golden_batch(z, call)
+        torch.manual_seed(seed)
+        agent.update(s, a, r, lp, ns, d)
+        log = agent.last_update_log.cpu().numpy()
+        want = z[f"u{call}/log"]
+        assert log.shape == want.shape
+        np.testing.assert_allclose(log, want, rtol=2e-4, atol=2e-5, err_msg=f"update {call} log")
+        np.testing.assert_allclose(agent.reward_normalizer.stats.cpu().numpy(),
+                                   [z[f"u{call}/rn_mean"], z[f"u{call}/rn_var"], z[f"u{call}/rn_count"]], rtol=1e-7)
+        assert float(agent.actor_optimizer.param_groups[0]["lr"]) == pytest.approx(float(z[f"u{call}/actor_lr"]))
+    for k, v in _params(agent).items():
+        flat = v.reshape(-1).cpu().numpy()
+        np.testing.assert_allclose(flat[sample_index(flat.size)], z["final/" + k], atol=5e-6, rtol=0, err_msg=k)
+
+
+def test_select_actions_numpy_and_tensor(ppo, tmp_path):
+    z = golden()
+    agent = _agent(ppo, z, tmp_path)
+    s, *_ = golden_batch(z, 0)
+    a_np, lp_np = agent.select_actions(s)
+    assert isinstance(a_np, np.ndarray) and a_np.shape == (s.shape[0], 45) and lp_np.shape == (s.shape[0],)
+    a_t, lp_t = agent.select_actions(dev(s))
+    assert a_t.is_cuda and lp_t.is_cuda
+    with torch.no_grad():
+        want = agent.actor(dev(s)).log_prob(a_t).sum(1)
+    torch.testing.assert_close(lp_t, want, rtol=1e-5, atol=1e-4)
+
+
+def test_checkpoint_round_trip(ppo, tmp_path):
+    z = golden()
+    a1 = _agent(ppo, z, tmp_path)
+    s, a, r, lp, ns, d = golden_batch(z, 0)
+    torch.manual_seed(1)
+    a1.update(s, a, r, lp, ns, d)
+    path = a1.save_checkpoint(5, {"episode_rewards": [[1.0]], "mean_rewards": [1.0]})
+    a2 = _agent(ppo, z, tmp_path)
+    a2.load_checkpoint(path)
+    for (k, v), (_, w) in zip(_params(a1).items(), _params(a2).items()):
+        assert torch.equal(v, w), k
+    assert torch.equal(a1.reward_normalizer.stats, a2.reward_normalizer.stats)
+    s, a, r, lp, ns, d = golden_batch(z, 1)
+    for ag in (a1, a2):
+        torch.manual_seed(2)
+        ag.update(s, a, r, lp, ns, d)
+    for (k, v), (_, w) in zip(_params(a1).items(), _params(a2).items()):
+        torch.testing.assert_close(v, w, rtol=0, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("reference_semantics", [True, False])
+def test_rollout_trainer_on_env(ppo, reference_semantics, tmp_path):
+    dp = importlib.import_module("diffusion-piano_amd")
+    env = dp.BatchedPianoEnv(64, dp.music.twinkle_twinkle_little_star_one_hand(), dp.TaskConfig(), device="cuda:0")
+    torch.manual_seed(0)
+    agent = ppo.PPOAgent(env.obs_dim, 45, batch_size=128, ppo_epochs=2, checkpoint_dir=str(tmp_path), use_wandb=False)
+    tr = ppo.RolloutTrainer(env, agent, horizon=4, reference_semantics=reference_semantics)
+    steps = sum(tr.iterate() for _ in range(3))
+    assert steps == 64 * (3 if reference_semantics else 12)
+    log = agent.last_update_log
+    assert torch.isfinite(log).all()
+    assert torch.isfinite(tr.ep_return).all()
+    env.close()
