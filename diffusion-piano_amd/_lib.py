@@ -19,7 +19,8 @@ EXPORTS = (
 )
 
 # Every entry point declared in include/pianorl.h.
-RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample")
+RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample",
+              "prl_clip_adam")
 
 _lib = None
 _rl = None
@@ -82,6 +83,7 @@ def load_rl() -> C.CDLL:
     L.prl_gae.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, i32, vp]
     L.prl_normalize.argtypes = [vp, i32, f32, vp]
     L.prl_gauss_sample.argtypes = [vp, vp, i32, i32, u64, u64, vp, vp, vp]
+    L.prl_clip_adam.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_int64), i32, vp, vp, f32, f32, f32, f32, vp, vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
     _rl = L

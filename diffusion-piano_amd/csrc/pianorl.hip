@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 
 #include "../../include/pianorl.h"
@@ -217,6 +218,78 @@ __global__ void __launch_bounds__(256) gauss_sample_kernel(const float* __restri
   if (lane == 0) logp[row] = lp;
 }
 
+// ---------------------------------------------------------------- clip_grad_norm_ + Adam
+// Flat fp32 buffers of every parameter (p, g, m, v), split into <= PRL_MAX_SEG contiguous
+// segments (one per network: the reference clips and steps actor and critic separately,
+// ppo_v2.py:280-293). Two launches replace torch's ~150 per minibatch (per-tensor norms,
+// foreach lerp/mul/addcmul/sqrt/div and the capturable bias corrections).
+constexpr int ADAM_PARTS = 256;  // partial-sum blocks of the norm pass
+constexpr int ADAM_THREADS = 256;
+
+struct Segs {
+  int64_t end[PRL_MAX_SEG];
+  int n;
+};
+
+__device__ __forceinline__ int64_t seg_begin(const Segs& sg, int s) { return s == 0 ? 0 : sg.end[s - 1]; }
+
+// pass 1: per-segment partial sums of g^2 (fp64), one row of partials per block; block 0
+// also advances the per-segment step counters (torch's state["step"] += 1)
+__global__ void __launch_bounds__(ADAM_THREADS) grad_sumsq_kernel(const float* __restrict__ g, Segs sg,
+                                                                  double* __restrict__ part, float* __restrict__ step) {
+  __shared__ double red[ADAM_THREADS / 64];
+  for (int s = 0; s < sg.n; s++) {
+    double acc = 0.0;
+    for (int64_t i = seg_begin(sg, s) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.end[s];
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const double x = (double)g[i];
+      acc += x * x;
+    }
+    const double tot = block_sum_d(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x * PRL_MAX_SEG + s] = tot;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < sg.n) step[threadIdx.x] += 1.f;
+}
+
+// pass 2: every block folds the partials into the clip coefficient of each segment
+// (torch.nn.utils.clip_grad_norm_: coef = min(1, max_norm / (||g|| + 1e-6))), then the Adam
+// update (torch.optim.Adam, amsgrad/weight_decay off) over a grid-stride range
+__global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                                 float* __restrict__ m, float* __restrict__ v, Segs sg,
+                                                                 const double* __restrict__ part,
+                                                                 const float* __restrict__ lr,
+                                                                 const float* __restrict__ step, float b1, float b2,
+                                                                 float eps, float max_norm, int nparts) {
+  __shared__ double red[ADAM_THREADS / 64];
+  __shared__ float coef[PRL_MAX_SEG], ssz[PRL_MAX_SEG], ibc2[PRL_MAX_SEG];
+  for (int s = 0; s < sg.n; s++) {
+    double acc = 0.0;
+    for (int b = threadIdx.x; b < nparts; b += blockDim.x) acc += part[b * PRL_MAX_SEG + s];
+    const double tot = block_sum_d(acc, red);
+    if (threadIdx.x == 0) {
+      const float norm = (float)sqrt(tot);
+      coef[s] = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
+      const double t = (double)step[s];
+      const double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
+      ssz[s] = (float)((double)lr[s] / bc1);
+      ibc2[s] = (float)(1.0 / sqrt(bc2));
+    }
+  }
+  __syncthreads();
+  const int64_t n = sg.end[sg.n - 1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < PRL_MAX_SEG - 1; k++) s += (k + 1 < sg.n && i >= sg.end[k]) ? 1 : 0;
+    const float gi = g[i] * coef[s];
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= ssz[s] * mi / (sqrtf(vi) * ibc2[s] + eps);
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI
@@ -258,6 +331,30 @@ int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint
   if (!mean || !log_std || !action || !logp) return fail("prl_gauss_sample: null pointer");
   if (n <= 0 || a <= 0 || a > 64) return fail("prl_gauss_sample: need n > 0 and 0 < a <= 64");
   gauss_sample_kernel<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(mean, log_std, n, a, seed, offset, action, logp);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
+                  int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
+                  double* scratch, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !seg_end || !lr || !step || !scratch)
+    return fail("prl_clip_adam: null pointer");
+  if (nseg < 1 || nseg > PRL_MAX_SEG) return fail("prl_clip_adam: need 1 <= nseg <= PRL_MAX_SEG");
+  Segs sg{};
+  sg.n = nseg;
+  for (int s = 0; s < nseg; s++) {
+    sg.end[s] = seg_end[s];
+    if (sg.end[s] < (s ? sg.end[s - 1] : 0) || sg.end[s] <= 0) return fail("prl_clip_adam: segment ends must increase");
+  }
+  for (int s = nseg; s < PRL_MAX_SEG; s++) sg.end[s] = sg.end[nseg - 1];
+  const int64_t n = sg.end[nseg - 1];
+  const int parts = (int)std::min<int64_t>(ADAM_PARTS, (n + ADAM_THREADS - 1) / ADAM_THREADS);
+  grad_sumsq_kernel<<<parts, ADAM_THREADS, 0, (hipStream_t)stream>>>(grad, sg, scratch, step);
+  HIPCHK(hipGetLastError());
+  const int blocks = (int)std::min<int64_t>(1024, (n + ADAM_THREADS * 4 - 1) / (ADAM_THREADS * 4));
+  clip_adam_kernel<<<blocks, ADAM_THREADS, 0, (hipStream_t)stream>>>(param, grad, exp_avg, exp_avg_sq, sg, scratch, lr,
+                                                                    step, beta1, beta2, eps, max_norm, parts);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -40,6 +40,7 @@ There is no CPU fallback: the agent needs a ROCm GPU and libpianorl.so.
 
 from __future__ import annotations
 
+import ctypes as C
 import math
 import time
 import warnings
@@ -207,7 +208,7 @@ def loader_permutation(n: int) -> torch.Tensor:
     return torch.randperm(n, generator=g)
 
 
-# ---------------------------------------------------------------- gradient bucket (DP)
+# ---------------------------------------------------------------- flat parameter state
 class GradBucket:
     """One flat fp32 buffer holding the gradients of ``params`` (``p.grad`` are views), so
     data-parallel training does one all-reduce per minibatch instead of one per tensor."""
@@ -229,6 +230,79 @@ class GradBucket:
             self.flat.div_(ws)
 
 
+class FlatAdam(GradBucket):
+    """Parameters, gradients and Adam moments of several networks in four flat HBM buffers;
+    ``step()`` is ``clip_grad_norm_`` + ``Adam.step`` of every network in two launches
+    (``prl_clip_adam``). The torch optimisers given are kept for their ``param_groups``
+    (ReduceLROnPlateau writes their lr tensors, which are views of ``self.lr``) and
+    ``state_dict`` (their state tensors are views of the flat moments)."""
+
+    def __init__(self, optimizers, lrs, max_norm, betas=(0.9, 0.999), eps=1e-5):
+        if len(optimizers) > 4:
+            raise ValueError("FlatAdam: at most PRL_MAX_SEG = 4 networks")
+        self.optimizers = optimizers
+        segs = [[p for g in opt.param_groups for p in g["params"]] for opt in optimizers]
+        params = [p for seg in segs for p in seg]
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        self.param = torch.empty(n, dtype=torch.float32, device=dev)
+        o = 0
+        for p in params:  # parameters become views of the flat buffer
+            self.param[o:o + p.numel()].copy_(p.data.reshape(-1))
+            p.data = self.param[o:o + p.numel()].view_as(p)
+            o += p.numel()
+        super().__init__(params)
+        self.exp_avg = torch.zeros_like(self.param)
+        self.exp_avg_sq = torch.zeros_like(self.param)
+        self.seg_end = (C.c_int64 * len(segs))(*np.cumsum([sum(p.numel() for p in seg) for seg in segs]).tolist())
+        self.nseg = len(segs)
+        self.lr = torch.tensor([float(x) for x in lrs], dtype=torch.float32, device=dev)
+        self.step_count = torch.zeros(self.nseg, dtype=torch.float32, device=dev)
+        self.scratch = torch.zeros(256 * 4, dtype=torch.float64, device=dev)
+        self.betas, self.eps, self.max_norm = betas, eps, max_norm
+        for s, opt in enumerate(optimizers):
+            for g in opt.param_groups:
+                g["lr"] = self.lr[s]
+        self._bind_state()
+
+    def _views(self):
+        o = 0
+        for s, opt in enumerate(self.optimizers):
+            for g in opt.param_groups:
+                for p in g["params"]:
+                    yield s, p, slice(o, o + p.numel())
+                    o += p.numel()
+
+    def _bind_state(self):
+        for s, p, sl in self._views():
+            st = self.optimizers[s].state[p]
+            st["step"] = self.step_count[s]
+            st["exp_avg"] = self.exp_avg[sl].view_as(p)
+            st["exp_avg_sq"] = self.exp_avg_sq[sl].view_as(p)
+
+    def load_optimizer_states(self, state_dicts):
+        """``Adam.load_state_dict`` for each network, then re-point the loaded state into the
+        flat buffers (load_state_dict replaces the tensors)."""
+        for s, (opt, sd) in enumerate(zip(self.optimizers, state_dicts)):
+            opt.load_state_dict(sd)
+            for g in opt.param_groups:
+                self.lr[s].fill_(float(g["lr"]))
+                g["lr"] = self.lr[s]
+        for s, p, sl in self._views():
+            st = self.optimizers[s].state[p]
+            self.exp_avg[sl].copy_(st["exp_avg"].reshape(-1))
+            self.exp_avg_sq[sl].copy_(st["exp_avg_sq"].reshape(-1))
+            self.step_count[s].fill_(float(st["step"]))
+        self._bind_state()
+
+    def step(self):
+        b1, b2 = self.betas
+        _lib.check_rl(_lib.load_rl().prl_clip_adam(
+            self.param.data_ptr(), self.flat.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+            self.seg_end, self.nseg, self.lr.data_ptr(), self.step_count.data_ptr(), float(b1), float(b2),
+            float(self.eps), float(self.max_norm), self.scratch.data_ptr(), _stream()))
+
+
 # ---------------------------------------------------------------- the agent (ppo_v2.py:133-336)
 class PPOAgent:
     def __init__(self, state_dim, action_dim, lr=1e-4, gamma=0.99, epsilon=0.2, entropy_coef=0.01, value_coef=1.0,
@@ -244,15 +318,16 @@ class PPOAgent:
         self.distributed = process_group is not None or (
             torch.distributed.is_available() and torch.distributed.is_initialized()
             and torch.distributed.get_world_size() > 1)
+        # the torch optimisers carry the reference's settings, param_groups and state_dict
+        # format; their step is FlatAdam's fused kernel (critic segment first, then actor)
+        adam = dict(betas=(0.9, 0.999), eps=1e-5, capturable=True)
+        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=torch.tensor(float(lr)), **adam)
+        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=torch.tensor(float(lr) * 2), **adam)
+        self.flat = FlatAdam([self.critic_optimizer, self.actor_optimizer], [float(lr) * 2, float(lr)],
+                             max_norm=max_grad_norm, betas=(0.9, 0.999), eps=1e-5)
+        self.bucket = self.flat
         if self.distributed:  # identical replicas: rank 0's initial weights everywhere
-            for p in list(self.actor.parameters()) + list(self.critic.parameters()):
-                torch.distributed.broadcast(p.data, src=0, group=process_group)
-        self.bucket = GradBucket(list(self.critic.parameters()) + list(self.actor.parameters()))
-        adam = dict(betas=(0.9, 0.999), eps=1e-5, capturable=True, foreach=True)
-        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(),
-                                                lr=torch.tensor(float(lr), device=self.device), **adam)
-        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(),
-                                                 lr=torch.tensor(float(lr) * 2, device=self.device), **adam)
+            torch.distributed.broadcast(self.flat.param, src=0, group=process_group)
         self.actor_scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.actor_optimizer, mode="max", factor=0.5,
                                                                           patience=100)
         self.critic_scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.critic_optimizer, mode="min",
@@ -323,18 +398,14 @@ class PPOAgent:
         actor_loss = -torch.min(surr1, surr2).mean() - self.entropy_coef * entropy
         value_pred = self.critic(b_s).squeeze(-1)
         critic_loss = F.mse_loss(value_pred, b_ret)
-        self.critic_optimizer.zero_grad(set_to_none=False)
-        self.actor_optimizer.zero_grad(set_to_none=False)
+        self.flat.flat.zero_()
         critic_loss.backward()
         actor_loss.backward()
         log_row.copy_(torch.stack([actor_loss, critic_loss, entropy, value_pred.mean(), b_ret.mean(),
                                    b_adv.mean()]).detach())
 
     def _clip_step(self):
-        torch.nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad_norm, foreach=True)
-        self.critic_optimizer.step()
-        torch.nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad_norm, foreach=True)
-        self.actor_optimizer.step()
+        self.flat.step()  # clip_grad_norm_ + Adam.step of the critic, then of the actor
 
     def _eager_step(self, idx, log_row):
         self._forward_backward(idx, log_row)
@@ -481,8 +552,7 @@ class PPOAgent:
         ck = torch.load(path, map_location=self.device, weights_only=True)
         self.actor.load_state_dict(ck["actor_state_dict"])
         self.critic.load_state_dict(ck["critic_state_dict"])
-        self.actor_optimizer.load_state_dict(ck["actor_optimizer_state_dict"])
-        self.critic_optimizer.load_state_dict(ck["critic_optimizer_state_dict"])
+        self.flat.load_optimizer_states([ck["critic_optimizer_state_dict"], ck["actor_optimizer_state_dict"]])
         self.actor_scheduler.load_state_dict(ck["actor_scheduler_state_dict"])
         self.critic_scheduler.load_state_dict(ck["critic_scheduler_state_dict"])
         if "reward_normalizer" in ck:

@@ -16,6 +16,8 @@
  *                        env batch axis); E = envs gives the time-axis GAE of a rollout.
  *   prl_normalize     <- advantages = (a - a.mean()) / (a.std() + 1e-8) (ppo_v2.py:256),
  *                        unbiased std as torch.std.
+ *   prl_clip_adam     <- clip_grad_norm_(max_grad_norm) + optimizer.step() of each network
+ *                        (ppo_v2.py:280-293), fused over one flat parameter buffer.
  *   prl_gauss_sample  <- select_actions: Normal(mean, exp(clamp(log_std,-20,2))).sample() and
  *                        log_prob(actions).sum(1) (ppo_v2.py:70-74, 211-218). Counter-based
  *                        Philox4x32-10 keyed by (seed, offset, row, column).
@@ -31,6 +33,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define PRL_MAX_SEG 4 /* parameter segments of prl_clip_adam (one per network) */
 
 /* returns_mode of prl_gae */
 #define PRL_RETURNS_TD 0  /* ret = r + gamma * next_values * (1 - done)   (ppo_v2.py:234-237) */
@@ -54,6 +58,16 @@ int prl_normalize(float* x, int n, float eps, void* stream);
 /* mean[n, a] f32, log_std[a] f32 -> action[n, a], logp[n] (sum over a). a <= 64. */
 int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint64_t seed, uint64_t offset,
                      float* action, float* logp, void* stream);
+
+/* clip_grad_norm_ + Adam over flat fp32 buffers (ppo_v2.py:280-293: clip each network's
+ * gradient to max_norm, then its Adam step; torch.nn.utils.clip_grad_norm_ and
+ * torch.optim.Adam(betas, eps), amsgrad and weight decay off). param / grad / exp_avg /
+ * exp_avg_sq [n], n = seg_end[nseg-1]; segment s = [seg_end[s-1], seg_end[s]) (HOST array)
+ * has its own clip, lr[s] (device) and step[s] (device f32, incremented here);
+ * scratch: device f64 [256 * PRL_MAX_SEG]. max_norm <= 0 disables clipping. */
+int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
+                  int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
+                  double* scratch, void* stream);
 
 #ifdef __cplusplus
 }
