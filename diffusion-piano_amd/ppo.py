@@ -307,10 +307,20 @@ class FlatAdam(GradBucket):
 class PPOAgent:
     def __init__(self, state_dim, action_dim, lr=1e-4, gamma=0.99, epsilon=0.2, entropy_coef=0.01, value_coef=1.0,
                  max_grad_norm=0.5, ppo_epochs=10, batch_size=64, device="cuda", checkpoint_dir="checkpoints",
-                 use_wandb=True, *, gae_lambda=0.95, process_group=None, graphs=True, sample_seed=None):
+                 use_wandb=True, *, gae_lambda=0.95, process_group=None, graphs=True, sample_seed=None,
+                 tune_gemms=False):
         if not torch.cuda.is_available():
             raise _lib.PianosimError("PPOAgent needs a ROCm GPU (torch.cuda.is_available() is False)")
         _lib.load_rl()  # fail loudly if the kernels are missing
+        if tune_gemms:
+            # TunableOp: the first call of each GEMM shape times the rocBLAS and hipBLASLt
+            # solutions and keeps the fastest (the minibatch GEMMs are M = 128 problems the
+            # default heuristics serve with 256-wide macro tiles). Every shape of the captured
+            # step is first met in the eager warm-up steps, so no tuning runs during capture.
+            import torch.cuda.tunable as tunable
+            tunable.enable(True)
+            tunable.tuning_enable(True)
+            tunable.set_max_tuning_duration(30)
         self.device = torch.device(device if str(device).startswith("cuda") else "cuda")
         self.actor = Actor(state_dim, action_dim).to(self.device)
         self.critic = Critic(state_dim).to(self.device)

@@ -43,9 +43,13 @@ def main():
     p.add_argument("--epochs", type=int, default=10)
     p.add_argument("--horizon", type=int, default=16)
     p.add_argument("--eager", action="store_true")
+    p.add_argument("--blas", default="default", choices=["default", "rocblas", "hipblaslt"])
+    p.add_argument("--no-tune", action="store_true", help="no TunableOp GEMM selection")
     args = p.parse_args()
 
     import torch
+    if args.blas != "default":
+        torch.backends.cuda.preferred_blas_library("cublas" if args.blas == "rocblas" else "cublaslt")
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,7 +70,7 @@ def main():
     torch.manual_seed(0)
     agent = ppo.PPOAgent(env.obs_dim, 45, lr=1e-4, gamma=0.99, epsilon=0.2, batch_size=args.batch,
                          ppo_epochs=args.epochs, checkpoint_dir="/tmp/ppo_bench_ckpt", use_wandb=False,
-                         graphs=not args.eager, sample_seed=1000 + rank)
+                         graphs=not args.eager, sample_seed=1000 + rank, tune_gemms=not args.no_tune)
     tr = ppo.RolloutTrainer(env, agent, horizon=args.horizon, reference_semantics=args.mode == "reference")
     for _ in range(args.warmup):
         tr.iterate()
@@ -115,6 +119,7 @@ def main():
                        "mode": args.mode, "envs_per_gpu": args.envs, "batch": args.batch, "epochs": args.epochs,
                        "horizon": args.horizon if args.mode == "rollout" else 1,
                        "minibatch_steps_per_update": nmb * args.epochs, "graphs": not args.eager,
+                       "blas": args.blas, "tunableop": not args.no_tune,
                        "parallelism": f"dp{world}"},
             "phases_ms": {"env_step": t_env * 1e3, "select_actions": t_sel * 1e3,
                           "update_host_wall": upd / args.iters * 1e3},
