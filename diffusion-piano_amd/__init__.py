@@ -4,8 +4,9 @@ Import with ``importlib.import_module("diffusion-piano_amd")`` (the directory na
 package name required by the build layout).
 """
 
-from . import abi, music, model  # noqa: F401
+from . import abi, music, model, evaluation  # noqa: F401
 from .envs import (  # noqa: F401
     Array, BatchedPianoEnv, BoundedArray, DEBUG, Environment, StepType, TaskConfig, TimeStep,
     VectorizedPianoEnv, compile_task, load, obs_layout,
 )
+from .evaluation import MidiEvaluationWrapper  # noqa: F401,E402

@@ -15,7 +15,7 @@ RL_LIB_PATH = Path(os.environ.get("PIANORL_LIB", HERE / "libpianorl.so"))
 EXPORTS = (
     "ps_last_error", "ps_version", "ps_obs_dim", "ps_model_desc_size", "ps_create", "ps_destroy",
     "ps_reset", "ps_step", "ps_get_state", "ps_set_state", "ps_set_applied", "ps_reward_terms",
-    "ps_fingertips", "ps_contact_count",
+    "ps_fingertips", "ps_contact_count", "ps_musical_metrics",
 )
 
 # Every entry point declared in include/pianorl.h.
@@ -53,6 +53,7 @@ def load() -> C.CDLL:
     L.ps_reward_terms.argtypes = [vp, vp, vp]
     L.ps_fingertips.argtypes = [vp, vp, vp]
     L.ps_contact_count.argtypes = [vp, vp, vp]
+    L.ps_musical_metrics.argtypes = [vp, vp, vp, vp]
     for name in EXPORTS:
         if name not in ("ps_last_error", "ps_version", "ps_model_desc_size", "ps_destroy"):
             getattr(L, name).restype = i32

@@ -18,6 +18,7 @@ MAX_NOTES = 16
 MAX_CONTACTS_LIMIT = 24
 MAX_ROWS = 64
 NTERMS = 5
+NMUSIC = 6  # ps_musical_metrics slots: precision, recall, f1, sustain_precision, sustain_recall, sustain_f1
 FIRST, MID, LAST = 0, 1, 2
 
 d = C.c_double

@@ -43,6 +43,8 @@ struct ps_env {
   int *d_count, *d_keys, *d_fingers;
   float *qpos, *qvel, *qws, *ctrl, *sustain, *applied, *terms, *tips;
   int *t_idx, *ncon;
+  float *mus_acc, *mus_ep;  // MidiEvaluationWrapper: running sums of this episode, last episode
+  int* mus_cnt;             // finished episodes per env
   uint8_t* last;
   bool applied_on;
 };
@@ -386,6 +388,9 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMalloc(&E->tips, sizeof(float) * N * 2 * PS_NFINGER * 3));
   HIPCHK(hipMalloc(&E->t_idx, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->ncon, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->mus_acc, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMalloc(&E->mus_ep, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMalloc(&E->mus_cnt, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->last, N));
   HIPCHK(hipMemset(E->qpos, 0, sizeof(float) * N * NV));
   HIPCHK(hipMemset(E->qvel, 0, sizeof(float) * N * NV));
@@ -397,6 +402,9 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMemset(E->tips, 0, sizeof(float) * N * 2 * PS_NFINGER * 3));
   HIPCHK(hipMemset(E->t_idx, 0, sizeof(int) * N));
   HIPCHK(hipMemset(E->ncon, 0, sizeof(int) * N));
+  HIPCHK(hipMemset(E->mus_acc, 0, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMemset(E->mus_ep, 0, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMemset(E->mus_cnt, 0, sizeof(int) * N));
   HIPCHK(hipMemset(E->last, 0, N));
   HIPCHK(hipDeviceSynchronize());
   E->applied_on = false;
@@ -410,6 +418,7 @@ void ps_destroy(ps_env* E) {
   hipFree(E->d_model); hipFree(E->d_goal); hipFree(E->d_count); hipFree(E->d_keys); hipFree(E->d_fingers);
   hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
+  hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt);
   delete E;
 }
 
@@ -421,7 +430,7 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
           (float)E->cfg.energy_penalty_coef, 0};
   if (const char* sk = getenv("PIANOSIM_SKIP")) cfg.skip = atoi(sk);
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
-         E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon};
+         E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt};
   hipLaunchKernelGGL(pianosim_kernel, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b, action,
                      mask, obs, reward, discount, step_type, mode, E->n);
   HIPCHK(hipGetLastError());
@@ -515,6 +524,16 @@ int ps_debug_timing(ps_env* E, uint64_t* out) {
   return 0;
 }
 #endif
+
+int ps_musical_metrics(ps_env* E, float* episode, int32_t* episodes, void* stream) {
+  if (!E) return fail("null argument");
+  if (episode)
+    HIPCHK(hipMemcpyAsync(episode, E->mus_ep, sizeof(float) * E->n * PS_NMUSIC, hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
+  if (episodes)
+    HIPCHK(hipMemcpyAsync(episodes, E->mus_cnt, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
 
 int ps_contact_count(ps_env* E, int32_t* ncon, void* stream) {
   if (!E || !ncon) return fail("null argument");

@@ -337,6 +337,14 @@ __device__ __forceinline__ float impedance(const float* si, float pos) {
   return clampf(imp, MINIMP, MAXIMP);
 }
 
+// sklearn precision_recall_fscore_support(average="binary", zero_division=1) from counts:
+// P = tp / (tp + fp), R = tp / (tp + fn), F = 2 tp / (2 tp + fp + fn), 1 where 0 / 0
+__device__ __forceinline__ void prf(int tp, int fp, int fn, float* out) {
+  out[0] = tp + fp ? (float)tp / (float)(tp + fp) : 1.f;
+  out[1] = tp + fn ? (float)tp / (float)(tp + fn) : 1.f;
+  out[2] = 2 * tp + fp + fn ? (float)(2 * tp) / (float)(2 * tp + fp + fn) : 1.f;
+}
+
 __device__ __forceinline__ float tolerance(float x, float lo, float hi, float margin) {
   if (x >= lo && x <= hi) return 1.f;
   float dd = (x < lo ? lo - x : x - hi) / margin;

@@ -274,6 +274,16 @@ class BatchedPianoEnv:
         _lib.check(_lib.load().ps_contact_count(self._h, t.data_ptr(), self.stream))
         return t
 
+    def musical_metrics(self):
+        """-> (episode [N, 6] f32, episodes [N] i32): each env's last finished episode's mean
+        precision / recall / F1 / sustain_precision / sustain_recall / sustain_f1
+        (MidiEvaluationWrapper, wrappers/evaluation.py:114-177) and its finished-episode count."""
+        torch = self._torch
+        ep = torch.empty(self.num_envs, abi.NMUSIC, device=self.device)
+        cnt = torch.empty(self.num_envs, device=self.device, dtype=torch.int32)
+        _lib.check(_lib.load().ps_musical_metrics(self._h, ep.data_ptr(), cnt.data_ptr(), self.stream))
+        return ep, cnt
+
     def obs_dict(self, obs=None) -> Dict[str, Any]:
         obs = self.obs if obs is None else obs
         return {k: obs[:, s] for k, s in self.obs_slices.items()}

@@ -24,6 +24,9 @@
  *                       physics.set_state).
  *   ps_set_applied   <- physics.bind(joints).qfrc_applied (piano_with_shadow_hands_test.py:239).
  *   ps_reward_terms  <- CompositeReward.reward_terms (composite_reward.py:62-64).
+ *   ps_musical_metrics <- MidiEvaluationWrapper (wrappers/evaluation.py:37-177): per-step
+ *                       precision / recall / F1 of the key and sustain activations against
+ *                       the notes of the step, averaged over each finished episode.
  *
  * Conventions: all array arguments of ps_reset/ps_step/ps_get_state/ps_set_state are
  * DEVICE pointers (e.g. torch-ROCm tensors' data_ptr()) and the calls are asynchronous
@@ -171,6 +174,15 @@ typedef struct {
 #define PS_TERM_FOREARM 4
 #define PS_NTERMS 5
 
+/* Slots of ps_musical_metrics (MidiEvaluationWrapper.get_musical_metrics keys). */
+#define PS_MUS_PRECISION 0
+#define PS_MUS_RECALL 1
+#define PS_MUS_F1 2
+#define PS_MUS_SUSTAIN_PRECISION 3
+#define PS_MUS_SUSTAIN_RECALL 4
+#define PS_MUS_SUSTAIN_F1 5
+#define PS_NMUSIC 6
+
 typedef struct ps_env ps_env;
 
 const char* ps_last_error(void);
@@ -207,6 +219,12 @@ int ps_reward_terms(ps_env* env, float* terms, void* stream);
 int ps_fingertips(ps_env* env, float* xpos, void* stream);
 /* Number of contacts after the last step/reset, [N]. */
 int ps_contact_count(ps_env* env, int32_t* ncon, void* stream);
+
+/* Musical metrics of each env's LAST finished episode, [N][PS_NMUSIC] (per-step binary
+ * precision / recall / F1 with zero_division = 1, as sklearn's precision_recall_fscore_support
+ * in evaluation.py:114-177, averaged over the episode's steps), and the number of episodes
+ * each env has finished since ps_create, [N]. Device pointers; either may be NULL. */
+int ps_musical_metrics(ps_env* env, float* episode, int32_t* episodes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -144,6 +144,10 @@ typedef struct {
   /* state */
   double q[NV], v[NV], qacc_ws[NV], ctrl[PS_NU], sustain, applied[NV];
   int t_idx, last;
+  /* MidiEvaluationWrapper (wrappers/evaluation.py): sums of the per-step metrics of the
+   * running episode, the last finished episode's means, finished-episode count */
+  double mus_acc[PS_NMUSIC], mus_ep[PS_NMUSIC];
+  int mus_cnt;
   /* kinematics */
   m3 R[NH][NB];
   v3 o[NH][NB], com[NH][NB], axis[NH][ND];
@@ -937,7 +941,27 @@ static void reset_env(ref_env* R, envdata* E, float* obs) {
   collide(&R->m, &R->cfg, E);
   key_state(&R->m, E);
   memset(E->terms, 0, sizeof(E->terms));
+  memset(E->mus_acc, 0, sizeof(E->mus_acc));
   if (obs) write_obs(R, E, obs, 0);
+}
+
+/* sklearn.metrics.precision_recall_fscore_support(y_true, y_pred, average="binary",
+ * zero_division=1) as the wrapper calls it (evaluation.py:135-140, 162-164): P = tp/(tp+fp),
+ * R = tp/(tp+fn), F = 2tp/(2tp+fp+fn) (sklearn >= 1.3 form), each 1 when its denominator is 0 */
+static void prf_counts(int tp, int fp, int fn, double* out) {
+  out[0] = tp + fp ? (double)tp / (tp + fp) : 1.0;
+  out[1] = tp + fn ? (double)tp / (tp + fn) : 1.0;
+  out[2] = 2 * tp + fp + fn ? (double)(2 * tp) / (2 * tp + fp + fn) : 1.0;
+}
+
+void ref_prf(const uint8_t* y_true, const uint8_t* y_pred, int n, double* out) {
+  int tp = 0, fp = 0, fn = 0;
+  for (int i = 0; i < n; i++) {
+    tp += y_true[i] && y_pred[i];
+    fp += !y_true[i] && y_pred[i];
+    fn += y_true[i] && !y_pred[i];
+  }
+  prf_counts(tp, fp, fn, out);
 }
 
 static void control_step(ref_env* R, envdata* E, const float* a, float* obs, float* rew, float* disc, uint8_t* st) {
@@ -962,6 +986,21 @@ static void control_step(ref_env* R, envdata* E, const float* a, float* obs, flo
   int terminal = t_new == R->T;
   int failure = 0;
   for (int k = 0; k < NK; k++) if (gc[k] == 0.0f && E->activation[k]) failure = 1;
+  /* MidiEvaluationWrapper.step (evaluation.py:65-86): ground truth = keys of the notes of
+   * step t_cur (task._notes, the goal row) and task._sustains[t_cur]; prediction = the
+   * piano's activation / sustain_activation after the step */
+  {
+    int tp = 0, fp = 0, fn = 0;
+    for (int k = 0; k < NK; k++) {
+      int g = gc[k] != 0.0f, a = E->activation[k] != 0;
+      tp += g && a; fp += !g && a; fn += g && !a;
+    }
+    double m[PS_NMUSIC];
+    prf_counts(tp, fp, fn, m);
+    int sg = gc[NK] != 0.0f, sa = sustain_act;
+    prf_counts(sg && sa, !sg && sa, sg && !sa, m + 3);
+    for (int i = 0; i < PS_NMUSIC; i++) E->mus_acc[i] += m[i];
+  }
   /* rewards */
   double kp = 0;
   int non = 0;
@@ -1045,6 +1084,10 @@ static void control_step(ref_env* R, envdata* E, const float* a, float* obs, flo
   *disc = (float)discount;
   *st = terminal ? PS_LAST : PS_MID;
   E->last = terminal;
+  if (terminal) {  /* episode means (np.mean over the episode's steps, evaluation.py:142-144) */
+    for (int i = 0; i < PS_NMUSIC; i++) E->mus_ep[i] = E->mus_acc[i] / t_new;
+    E->mus_cnt += 1;
+  }
 }
 
 /* ------------------------------------------------------------------ API */
@@ -1139,6 +1182,13 @@ void ref_fingertips(const ref_env* R, double* xpos) {
         v3 p = site_pos(&R->m, &R->e[i], h, s);
         for (int c = 0; c < 3; c++) xpos[(((size_t)i * NH + h) * PS_NFINGER + s) * 3 + c] = p.v[c];
       }
+}
+
+void ref_musical_metrics(const ref_env* R, double* episode, int32_t* episodes) {
+  for (int i = 0; i < R->n; i++) {
+    if (episode) memcpy(episode + (size_t)i * PS_NMUSIC, R->e[i].mus_ep, sizeof(double) * PS_NMUSIC);
+    if (episodes) episodes[i] = R->e[i].mus_cnt;
+  }
 }
 
 void ref_contact_count(const ref_env* R, int32_t* ncon) {

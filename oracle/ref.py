@@ -47,6 +47,8 @@ def lib():
         L.ref_reward_terms.argtypes = [C.c_void_p, _f64p]
         L.ref_fingertips.argtypes = [C.c_void_p, _f64p]
         L.ref_contact_count.argtypes = [C.c_void_p, _i32p]
+        L.ref_musical_metrics.argtypes = [C.c_void_p, _f64p, _i32p]
+        L.ref_prf.argtypes = [_u8p, _u8p, C.c_int, _f64p]
         L.ref_physics_substep.argtypes = [C.c_void_p]
         L.ref_tolerance.restype = C.c_double
         L.ref_tolerance.argtypes = [C.c_double] * 4
@@ -139,8 +141,23 @@ class OracleEnv:
         lib().ref_contact_count(self._h, c)
         return c
 
+    def musical_metrics(self):
+        ep = np.zeros((self.n, 6))
+        cnt = np.zeros(self.n, np.int32)
+        lib().ref_musical_metrics(self._h, ep, cnt)
+        return ep, cnt
+
     def physics_substep(self):
         lib().ref_physics_substep(self._h)
+
+
+def prf(y_true, y_pred):
+    """Binary precision / recall / F1 (zero_division=1) of the oracle (evaluation.py:135-140)."""
+    yt = np.ascontiguousarray(np.asarray(y_true) != 0, np.uint8)
+    yp = np.ascontiguousarray(np.asarray(y_pred) != 0, np.uint8)
+    out = np.zeros(3)
+    lib().ref_prf(yt, yp, yt.size, out)
+    return out
 
 
 def tolerance(x, lo, hi, margin):
