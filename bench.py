@@ -104,10 +104,16 @@ def drift_summary():
     if not d:
         return None
     out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"), "song": d.get("song")}
+    chaos = _profile("chaos_floor.json") or {}
     for k in ("zero_action", "trace_actions", "random_actions"):
         if k in d:
             out[k] = {"teacher_forced_p99": d[k]["teacher_forced_qpos_linf"]["p99"],
                       "free_running_1000_steps_max": d[k]["free_running_max_over_1000"]}
+            # the same metric for the fp64 checker against itself, 1e-12 perturbation per
+            # episode (tools/chaos_floor.py): the floor any non-bit-identical run sits on
+            c = chaos.get(f"{k.split('_')[0]}/delta=1e-12")
+            if c:
+                out[k]["fp64_self_1e-12_free_running_max"] = c["max_over_1000"]
     return out
 
 

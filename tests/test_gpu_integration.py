@@ -39,3 +39,19 @@ def test_raw_ctypes_snippet(dp):
         assert (ns["stype"] == 1).all()
     finally:
         os.chdir(cwd)
+
+
+def test_ppo_snippets(dp):
+    ns = {}
+    exec(_blocks()[2], ns)
+    assert ns["PPOAgent"].__module__.endswith(".ppo")
+    ns = {}
+    exec(_blocks()[3], ns)
+    log = ns["agent"].last_update_log
+    assert log is not None and torch.isfinite(log).all()
+    env, ev = ns["env"], ns["evaluator"]
+    act = torch.zeros(256, 45, device="cuda:0")
+    for _ in range(161):
+        ev.step(act)
+    m = ev.get_musical_metrics()
+    assert 0.0 <= m["f1"] <= 1.0
