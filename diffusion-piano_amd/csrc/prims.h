@@ -107,12 +107,13 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
 __device__ __forceinline__ int lanes_below(uint64_t mask, int lane) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
 }
-// exclusive prefix sum and total of small non-negative counts (< 32) by bit-plane ballots:
-// 5 ballots + mbcnt, no cross-lane data movement
+// exclusive prefix sum and total of small non-negative counts (< 2^BITS) by bit-plane
+// ballots: BITS ballots + mbcnt, no cross-lane data movement
+template <int BITS = 5>
 __device__ __forceinline__ int small_excl_scan(int v, int lane, int* total) {
   int ex = 0, tot = 0;
 #pragma unroll
-  for (int b = 0; b < 5; b++) {
+  for (int b = 0; b < BITS; b++) {
     const uint64_t m = __ballot((v >> b) & 1);
     ex += lanes_below(m, lane) << b;
     tot += __popcll(m) << b;
