@@ -245,8 +245,11 @@ __device__ __forceinline__ float seg_box_t(f3 a3, f3 d3, const float* hs) {
   return bestt;
 }
 
-// capsule (geom2) vs box (geom1); writes up to 2 contacts at out (if non-null), returns count
-__device__ int capsule_box(f3 p0, f3 p1, float r, f3 c, const float* R, const float* hs, Contact* out, int slot,
+// capsule (geom2) vs box (geom1); writes up to 2 contacts at out (if non-null), returns count.
+// Not inlined: its four call sites (count / write pass, substep / task layer) would each
+// carry a copy of the segment-box search, and the kernel is instruction-cache bound enough
+// that one shared copy measures ~2% faster (tools/throughput.py A/B on MI355X).
+__device__ __noinline__ int capsule_box(f3 p0, f3 p1, float r, f3 c, const float* R, const float* hs, Contact* out, int slot,
                            int maxc, int kind, int key, int g2) {
   int n = 0;
   f3 nrm, pos;

@@ -17,12 +17,12 @@ L.ps_debug_timing(g._h, None)
 gen = torch.Generator(device="cuda:0").manual_seed(1)
 for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
-out = np.zeros((N, 16), np.uint64)
+out = np.zeros((N, 18), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
 names = {0: "kinematics", 1: "dynamics", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
          3: "factor", 4: "solve_smooth",
          12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T", 15: "cons:finish",
-         8: "pgs", 6: "integrate", 5: "final+task"}
+         16: "pgs:build A", 17: "pgs:sweeps", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
 for i, n in names.items():
     v = out[:, i].astype(np.float64)

@@ -22,13 +22,18 @@ def throughput(name, n, steps=20):
     acts = [torch.rand(n, 45, device="cuda:0", generator=gen) * 2 - 1 for _ in range(steps)]
     for i in range(3):
         g.step(acts[i])
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        g.step(acts[i])
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    print(f"{name:15s} N={n:6d}: {n * steps / dt:12,.0f} env-steps/s ({dt / steps * 1e3:.2f} ms/step)", flush=True)
+    rates = []
+    for _ in range(5):  # median of 5 timed blocks (the box's clocks wander by a few %)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            g.step(acts[i])
+        torch.cuda.synchronize()
+        rates.append(n * steps / (time.perf_counter() - t0))
+    r = sorted(rates)[2]
+    lib = Path(dp._lib.LIB_PATH).name
+    print(f"{name:15s} N={n:6d}: {r:12,.0f} env-steps/s ({n / r * 1e3:.3f} ms/step) "
+          f"[min {min(rates):,.0f} max {max(rates):,.0f}] {lib}", flush=True)
 
 
 if __name__ == "__main__":
