@@ -91,6 +91,41 @@ def load_rl() -> C.CDLL:
     return L
 
 
+SONG_LIB_PATH = Path(os.environ.get("PIANOSONG_LIB", HERE / "libpianosong.so"))
+# Every entry point declared in include/pianosong.h.
+SONG_EXPORTS = ("pss_last_error", "pss_version", "pss_parse_midi", "pss_from_notes", "pss_free", "pss_info",
+                "pss_get", "pss_add_fingering", "pss_trim_silence", "pss_song_tables")
+_song = None
+
+
+def load_song() -> C.CDLL:
+    """libpianosong.so: native MIDI / fingering ingestion (include/pianosong.h, host only)."""
+    global _song
+    if _song is not None:
+        return _song
+    if not SONG_LIB_PATH.exists():
+        raise PianosimError(
+            f"{SONG_LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(SONG_LIB_PATH))
+    vp, i32, f64 = C.c_void_p, C.c_int, C.c_double
+    L.pss_last_error.restype = C.c_char_p
+    L.pss_version.restype = i32
+    L.pss_parse_midi.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
+    L.pss_from_notes.argtypes = [vp, i32, vp, i32, f64, C.POINTER(vp)]
+    L.pss_free.argtypes = [vp]
+    L.pss_free.restype = None
+    L.pss_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(f64), C.POINTER(i32)]
+    L.pss_get.argtypes = [vp, vp, vp]
+    L.pss_add_fingering.argtypes = [vp, C.c_char_p]
+    L.pss_trim_silence.argtypes = [vp]
+    L.pss_song_tables.argtypes = [vp, f64, f64, i32, i32, vp, vp, vp, vp, C.POINTER(i32)]
+    for name in SONG_EXPORTS[2:]:
+        if name != "pss_free":
+            getattr(L, name).restype = i32
+    _song = L
+    return L
+
+
 def check_rl(rc: int) -> None:
     if rc != 0:
         msg = load_rl().prl_last_error()

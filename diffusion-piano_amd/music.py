@@ -1,7 +1,9 @@
 """Song ingestion for the batched piano environment (host precompute, init-time only).
 
-Restates, without note_seq / pretty_midi (absent on the GPU box), the pieces of the
-reference's music pipeline that feed the hot path:
+The reference's music pipeline (note_seq / pretty_midi in Python, both absent on the GPU
+box) restated natively in ``libpianosong.so`` (``csrc/song.cpp``, C-ABI
+``include/pianosong.h``); this module is its Python face and keeps the reference's data
+classes:
 
 * Standard MIDI File parsing with pretty_midi's note-pairing semantics
   (used by ``note_seq.midi_io.midi_file_to_note_sequence``, called at
@@ -15,18 +17,20 @@ reference's music pipeline that feed the hot path:
 
 The product of this module is a :class:`SongTables` object: the dense per-control-step
 goal table ``[T, 89]`` plus per-step (key, finger) lists that the GPU kernel reads.
+Malformed input raises ``ValueError`` with the library's message.
 """
 
 from __future__ import annotations
 
-import math
+import ctypes as C
 import re
-import struct
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
+
+from . import _lib
 
 MIN_MIDI_PITCH_PIANO = 21  # robopianist/music/constants.py:21
 MAX_MIDI_PITCH_PIANO = 108
@@ -69,22 +73,74 @@ class NoteSequence:
 
 
 # ---------------------------------------------------------------------------------------
-# Standard MIDI File parsing (pretty_midi semantics).
+# libpianosong.so (include/pianosong.h)
 # ---------------------------------------------------------------------------------------
 
 
-def _read_varlen(data: bytes, pos: int) -> Tuple[int, int]:
-    value = 0
-    while True:
-        b = data[pos]
-        pos += 1
-        value = (value << 7) | (b & 0x7F)
-        if not b & 0x80:
-            return value, pos
+class _PssNote(C.Structure):
+    _fields_ = [("pitch", C.c_int32), ("start_time", C.c_double), ("end_time", C.c_double),
+                ("velocity", C.c_int32), ("part", C.c_int32)]
+
+
+class _PssCC(C.Structure):
+    _fields_ = [("time", C.c_double), ("control_number", C.c_int32), ("control_value", C.c_int32)]
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = _lib.load_song().pss_last_error()
+        raise ValueError(msg.decode() if msg else f"pianosong error {rc}")
+
+
+class _Seq:
+    """Owns a pss_seq handle."""
+
+    def __init__(self, h: C.c_void_p):
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            _lib.load_song().pss_free(self.h)
+            self.h = None
+
+    @classmethod
+    def parse(cls, data: bytes) -> "_Seq":
+        h = C.c_void_p()
+        buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+        _check(_lib.load_song().pss_parse_midi(buf, len(data), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def of(cls, seq: NoteSequence) -> "_Seq":
+        notes = (_PssNote * max(1, len(seq.notes)))(*[_PssNote(n.pitch, n.start_time, n.end_time, n.velocity, n.part)
+                                                      for n in seq.notes])
+        ccs = (_PssCC * max(1, len(seq.control_changes)))(
+            *[_PssCC(c.time, c.control_number, c.control_value) for c in seq.control_changes])
+        h = C.c_void_p()
+        _check(_lib.load_song().pss_from_notes(notes, len(seq.notes), ccs, len(seq.control_changes),
+                                               float(seq.total_time), C.byref(h)))
+        return cls(h)
+
+    def sequence(self, title: str) -> NoteSequence:
+        L = _lib.load_song()
+        nn, nc, tt = C.c_int(), C.c_int(), C.c_double()
+        _check(L.pss_info(self.h, C.byref(nn), C.byref(nc), C.byref(tt), None))
+        notes = (_PssNote * max(1, nn.value))()
+        ccs = (_PssCC * max(1, nc.value))()
+        _check(L.pss_get(self.h, notes, ccs))
+        seq = NoteSequence(title=title, total_time=tt.value)
+        seq.notes = [Note(n.pitch, n.start_time, n.end_time, n.velocity, n.part) for n in notes[:nn.value]]
+        seq.control_changes = [ControlChange(c.time, c.control_number, c.control_value) for c in ccs[:nc.value]]
+        return seq
+
+
+# ---------------------------------------------------------------------------------------
+# The reference's functions
+# ---------------------------------------------------------------------------------------
 
 
 def parse_midi(path) -> NoteSequence:
-    """Parses a type-0/1 SMF into a :class:`NoteSequence`.
+    """Parses a type-0/1 SMF into a :class:`NoteSequence` (``pss_parse_midi``).
 
     Note pairing follows pretty_midi ``PrettyMIDI._load_instruments``: a note-off (or a
     note-on with velocity 0) closes every open note of that (channel, pitch) that started
@@ -93,151 +149,17 @@ def parse_midi(path) -> NoteSequence:
     instrument by instrument, which is the order note_seq copies them into the sequence.
     Ticks map to seconds through the merged tempo map (default 120 qpm).
     """
-    data = Path(path).read_bytes()
-    if data[:4] != b"MThd":
-        raise ValueError(f"{path}: not a Standard MIDI File")
-    hdr_len = struct.unpack(">I", data[4:8])[0]
-    fmt, ntracks, division = struct.unpack(">HHH", data[8:14])
-    if division & 0x8000:
-        raise ValueError("SMPTE time division is not supported")
-    pos = 8 + hdr_len
-
-    tracks = []  # list of [(abs_tick, kind, payload)]
-    for _ in range(ntracks):
-        if data[pos:pos + 4] != b"MTrk":
-            raise ValueError("bad track chunk")
-        length = struct.unpack(">I", data[pos + 4:pos + 8])[0]
-        p, end = pos + 8, pos + 8 + length
-        tick, status, events = 0, 0, []
-        while p < end:
-            delta, p = _read_varlen(data, p)
-            tick += delta
-            b = data[p]
-            if b == 0xFF:  # meta
-                mtype = data[p + 1]
-                mlen, p = _read_varlen(data, p + 2)
-                payload = data[p:p + mlen]
-                p += mlen
-                if mtype == 0x51:
-                    events.append((tick, "tempo", (payload[0] << 16) | (payload[1] << 8) | payload[2]))
-                elif mtype == 0x2F:
-                    break
-                continue
-            if b in (0xF0, 0xF7):  # sysex
-                slen, p = _read_varlen(data, p + 1)
-                p += slen
-                continue
-            if b & 0x80:
-                status = b
-                p += 1
-            kind = status & 0xF0
-            ch = status & 0x0F
-            if kind in (0xC0, 0xD0):
-                d1 = data[p]
-                p += 1
-                if kind == 0xC0:
-                    events.append((tick, "program", (ch, d1)))
-                continue
-            d1, d2 = data[p], data[p + 1]
-            p += 2
-            if kind == 0x90:
-                events.append((tick, "on" if d2 > 0 else "off", (ch, d1, d2)))
-            elif kind == 0x80:
-                events.append((tick, "off", (ch, d1, d2)))
-            elif kind == 0xB0:
-                events.append((tick, "cc", (ch, d1, d2)))
-        tracks.append(events)
-        pos = end
-
-    # Tempo map (pretty_midi reads tempo changes from every track).
-    tempos = sorted((t, v) for events in tracks for (t, k, v) in events if k == "tempo")
-    if not tempos or tempos[0][0] != 0:
-        tempos.insert(0, (0, 500000))
-    # Collapse same-tick changes: the last one wins.
-    tmap = []
-    for t, v in tempos:
-        if tmap and tmap[-1][0] == t:
-            tmap[-1] = (t, v)
-        else:
-            tmap.append((t, v))
-    seg_start_time = [0.0]
-    for i in range(1, len(tmap)):
-        dt_ticks = tmap[i][0] - tmap[i - 1][0]
-        seg_start_time.append(seg_start_time[-1] + dt_ticks * tmap[i - 1][1] / 1e6 / division)
-
-    def tick_to_time(tick: int) -> float:
-        i = len(tmap) - 1
-        while tmap[i][0] > tick:
-            i -= 1
-        return seg_start_time[i] + (tick - tmap[i][0]) * tmap[i][1] / 1e6 / division
-
-    instruments = {}  # (track, channel, program) -> list of notes, insertion ordered
-    ccs: List[ControlChange] = []
-    for ti, events in enumerate(tracks):
-        program = {}
-        open_notes = {}
-        for tick, kind, payload in events:
-            if kind == "program":
-                ch, prog = payload
-                program[ch] = prog
-            elif kind == "on":
-                ch, pitch, vel = payload
-                open_notes.setdefault((ch, pitch), []).append((tick, vel))
-            elif kind == "off":
-                ch, pitch, _ = payload
-                key = (ch, pitch)
-                if key not in open_notes:
-                    continue
-                to_close = [(s, v) for s, v in open_notes[key] if s != tick]
-                to_keep = [(s, v) for s, v in open_notes[key] if s == tick]
-                inst = instruments.setdefault((ti, ch, program.get(ch, 0)), [])
-                for s, v in to_close:
-                    inst.append(Note(pitch, tick_to_time(s), tick_to_time(tick), v))
-                if to_close and to_keep:
-                    open_notes[key] = to_keep
-                elif to_close:
-                    del open_notes[key]
-            elif kind == "cc":
-                ch, num, val = payload
-                ccs.append(ControlChange(tick_to_time(tick), num, val))
-    seq = NoteSequence(title=Path(path).stem)
-    for notes in instruments.values():
-        seq.notes.extend(notes)
-    seq.control_changes = ccs
-    seq.total_time = max([n.end_time for n in seq.notes] + [0.0])
-    return seq
+    return _Seq.parse(Path(path).read_bytes()).sequence(Path(path).stem)
 
 
 def trim_silence(seq: NoteSequence) -> NoteSequence:
-    """``MidiFile.trim_silence``: ``extract_subsequence(seq, notes[0].start, notes[-1].end)``.
-
-    note_seq semantics: notes are visited sorted by start time; notes starting inside
-    ``[start, end)`` are shifted by ``-start`` and their end clipped to ``end``; the total
-    time becomes the latest clipped end. Control changes inside the window are shifted;
-    a sustain pedal held at ``start`` is re-emitted at time 0.
-    """
-    if not seq.notes:
-        return NoteSequence(title=seq.title)
-    start, end = seq.notes[0].start_time, seq.notes[-1].end_time
-    out = NoteSequence(title=seq.title)
-    for n in sorted(seq.notes, key=lambda n: n.start_time):
-        if n.start_time < start or n.start_time >= end:
-            continue
-        e = min(n.end_time, end) - start
-        out.notes.append(Note(n.pitch, n.start_time - start, e, n.velocity, n.part))
-        out.total_time = max(out.total_time, e)
-    pedal_value = None
-    for cc in sorted(seq.control_changes, key=lambda c: c.time):
-        if cc.time < start:
-            if cc.control_number == SUSTAIN_PEDAL_CC_NUMBER:
-                pedal_value = cc.control_value
-            continue
-        if cc.time >= end:
-            continue
-        out.control_changes.append(ControlChange(cc.time - start, cc.control_number, cc.control_value))
-    if pedal_value is not None and pedal_value >= 64:
-        out.control_changes.insert(0, ControlChange(0.0, SUSTAIN_PEDAL_CC_NUMBER, pedal_value))
-    return out
+    """``MidiFile.trim_silence``: ``extract_subsequence(seq, notes[0].start, notes[-1].end)``
+    (``pss_trim_silence``): notes starting inside ``[start, end)`` shifted by ``-start``, ends
+    clipped to ``end``; control changes inside the window shifted; a sustain pedal held at
+    ``start`` re-emitted at time 0."""
+    s = _Seq.of(seq)
+    _check(_lib.load_song().pss_trim_silence(s.h))
+    return s.sequence(seq.title)
 
 
 _NOTE_VALUES = {
@@ -249,35 +171,21 @@ _NOTE_VALUES = {
 def parse_pitch_to_midi_number(pitch_str: str) -> int:
     """``data_processing/add_fingering_to_midi.py:7-24``."""
     m = re.match(r"([A-G][#b]?)(\d+)", pitch_str)
-    if not m:
+    if not m or m.group(1) not in _NOTE_VALUES:
         raise ValueError(f"Invalid pitch format: {pitch_str}")
     note, octave = m.groups()
     return _NOTE_VALUES[note] + (int(octave) + 1) * 12
 
 
 def add_fingering_from_annotation_file(midi_path, annotation_path) -> NoteSequence:
-    """``data_processing/add_fingering_to_midi.py:26-83``.
+    """``data_processing/add_fingering_to_midi.py:26-83`` (``pss_add_fingering``).
 
     Each sequence note takes the finger of the first annotation line whose start and end
     times are within 10 ms and whose pitch is equal.
     """
-    fingering = []
-    for line in Path(annotation_path).read_text().splitlines():
-        if line.startswith("//") or not line.strip():
-            continue
-        parts = line.strip().split("\t")
-        if len(parts) == 8:
-            _, start, end, pitch, _, _, _, finger = parts
-            f = int(finger)
-            if 0 <= f <= 9:
-                fingering.append((float(start), float(end), parse_pitch_to_midi_number(pitch), f))
-    seq = parse_midi(midi_path)
-    for note in seq.notes:
-        for s, e, p, f in fingering:
-            if abs(note.start_time - s) < 0.01 and abs(note.end_time - e) < 0.01 and note.pitch == p:
-                note.part = f
-                break
-    return seq
+    s = _Seq.parse(Path(midi_path).read_bytes())
+    _check(_lib.load_song().pss_add_fingering(s.h, Path(annotation_path).read_bytes()))
+    return s.sequence(Path(midi_path).stem)
 
 
 def twinkle_twinkle_little_star_one_hand() -> NoteSequence:
@@ -294,67 +202,8 @@ def twinkle_twinkle_little_star_one_hand() -> NoteSequence:
 
 
 # ---------------------------------------------------------------------------------------
-# NoteTrajectory.
+# NoteTrajectory / device tables.
 # ---------------------------------------------------------------------------------------
-
-
-def note_trajectory(seq: NoteSequence, dt: float):
-    """``NoteTrajectory.seq_to_trajectory`` (robopianist/music/midi_file.py:315-362).
-
-    Returns ``notes[T]`` as lists of ``(key, fingering)`` in increasing MIDI pitch order and
-    ``sustains[T]``. Frame semantics are those of ``sequence_to_pianoroll``
-    (robopianist/music/piano_roll.py:59-204) with ``onset_window=0``: a note occupies
-    frames ``[int(s*fps), max(start+1, ceil(e*fps)))``; a note whose onset frame re-strikes
-    a key that was active in the previous frame is dropped from that frame.
-    """
-    fps = 1.0 / dt
-    n_frames = int(seq.total_time * fps + 1)
-    vel = np.zeros((n_frames, 128), dtype=np.float32)
-    onset = np.zeros((n_frames, 128), dtype=np.float32)
-    finger = np.full((n_frames, 128), -1, dtype=np.float32)
-    cc = np.zeros((n_frames, 128), dtype=np.int32)
-
-    def frames(s, e):
-        sf = int(s * fps)
-        ef = int(math.ceil(e * fps))
-        return sf, max(sf + 1, ef)
-
-    for note in sorted(seq.notes, key=lambda n: n.start_time):
-        if note.pitch < 0 or note.pitch > 127:
-            continue
-        sf, ef = frames(note.start_time, note.end_time)
-        onset[sf:min(n_frames, sf + 1), note.pitch] = 1.0
-        vel[sf:ef, note.pitch] = note.velocity / MAX_VELOCITY
-        finger[sf:ef, note.pitch] = note.part
-    for c in seq.control_changes:
-        f, _ = frames(c.time, 0)
-        if f < n_frames:
-            cc[f, c.control_number] = c.control_value + 1
-    onset_vel = vel * onset
-
-    notes: List[List[Tuple[int, int]]] = []
-    for t in range(n_frames):
-        step = []
-        for idx in np.nonzero(vel[t])[0]:
-            if t > 0 and vel[t - 1][idx] and onset_vel[t][idx]:
-                continue
-            if not MIN_MIDI_PITCH_PIANO <= idx <= MAX_MIDI_PITCH_PIANO:
-                raise ValueError(f"pitch {idx} outside the piano range")
-            step.append((int(idx) - MIN_MIDI_PITCH_PIANO, int(finger[t, idx])))
-        notes.append(step)
-    sustains: List[int] = []
-    prev = 0
-    for t in range(n_frames):
-        ev = cc[t, SUSTAIN_PEDAL_CC_NUMBER]
-        if 1 <= ev <= SUSTAIN_PEDAL_CC_NUMBER:
-            s = 0
-        elif SUSTAIN_PEDAL_CC_NUMBER + 1 <= ev <= MAX_CC_VALUE + 1:
-            s = 1
-        else:
-            s = prev
-        sustains.append(s)
-        prev = s
-    return notes, sustains
 
 
 @dataclass
@@ -378,30 +227,42 @@ class SongTables:
         return int(self.goal.shape[0])
 
 
+def _tables(seq: NoteSequence, dt: float, initial_buffer_time: float, max_notes: int):
+    L = _lib.load_song()
+    s = _Seq.of(seq)
+    T = C.c_int()
+    _check(L.pss_song_tables(s.h, float(dt), float(initial_buffer_time), 0, max_notes, None, None, None, None,
+                             C.byref(T)))
+    n = T.value
+    goal = np.zeros((n, NUM_KEYS + 1), np.float32)
+    count = np.zeros(n, np.int32)
+    keys = np.full((n, max_notes), -1, np.int32)
+    fingers = np.full((n, max_notes), -1, np.int32)
+    _check(L.pss_song_tables(s.h, float(dt), float(initial_buffer_time), n, max_notes, goal.ctypes.data,
+                             count.ctypes.data, keys.ctypes.data, fingers.ctypes.data, C.byref(T)))
+    return goal, count, keys, fingers
+
+
+def note_trajectory(seq: NoteSequence, dt: float):
+    """``NoteTrajectory.seq_to_trajectory`` (robopianist/music/midi_file.py:315-362).
+
+    Returns ``notes[T]`` as lists of ``(key, fingering)`` in increasing MIDI pitch order and
+    ``sustains[T]``. Frame semantics are those of ``sequence_to_pianoroll``
+    (robopianist/music/piano_roll.py:59-204) with ``onset_window=0``: a note occupies
+    frames ``[int(s*fps), max(start+1, ceil(e*fps)))``; a note whose onset frame re-strikes
+    a key that was active in the previous frame is dropped from that frame.
+    """
+    goal, count, keys, fingers = _tables(seq, dt, 0.0, NUM_KEYS)
+    notes: List[List[Tuple[int, int]]] = [[(int(keys[t, i]), int(fingers[t, i])) for i in range(count[t])]
+                                          for t in range(len(count))]
+    return notes, [int(x) for x in goal[:, NUM_KEYS]]
+
+
 def song_tables(seq: NoteSequence, dt: float, initial_buffer_time: float = 0.0,
                 name: Optional[str] = None) -> SongTables:
-    """``PianoWithShadowHands._reset_trajectory`` (piano_with_shadow_hands.py:159-165)."""
-    notes, sustains = note_trajectory(seq, dt)
-    # NoteTrajectory.add_initial_buffer_time (midi_file.py:388-401).
-    if initial_buffer_time < 0:
-        raise ValueError("initial_buffer_time must be non-negative.")
-    nbuf = int(round(initial_buffer_time / dt))
-    notes = [[] for _ in range(nbuf)] + notes
-    sustains = [0] * nbuf + sustains
-    T = len(notes)
-    goal = np.zeros((T, NUM_KEYS + 1), dtype=np.float32)
-    count = np.zeros(T, dtype=np.int32)
-    keys = np.full((T, MAX_NOTES_PER_STEP), -1, dtype=np.int32)
-    fingers = np.full((T, MAX_NOTES_PER_STEP), -1, dtype=np.int32)
-    for t, step in enumerate(notes):
-        if len(step) > MAX_NOTES_PER_STEP:
-            raise ValueError(f"step {t} has {len(step)} notes > {MAX_NOTES_PER_STEP}")
-        count[t] = len(step)
-        for i, (k, f) in enumerate(step):
-            goal[t, k] = 1.0
-            keys[t, i] = k
-            fingers[t, i] = f
-        goal[t, NUM_KEYS] = sustains[t]
+    """``PianoWithShadowHands._reset_trajectory`` (piano_with_shadow_hands.py:159-165), with
+    ``NoteTrajectory.add_initial_buffer_time`` (midi_file.py:388-401)."""
+    goal, count, keys, fingers = _tables(seq, dt, initial_buffer_time, MAX_NOTES_PER_STEP)
     return SongTables(name or seq.title, goal, count, keys, fingers, seq.has_fingering())
 
 

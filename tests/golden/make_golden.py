@@ -33,8 +33,10 @@ import numpy as np
 REF = Path("/root/reference")
 ROOT = Path(__file__).resolve().parents[2]
 OUT = ROOT / "tests" / "golden"
-sys.path.insert(0, str(ROOT / "diffusion-piano_amd"))
-import music as our_music  # noqa: E402  (only for the .mid parse, see module docstring)
+sys.path.insert(0, str(ROOT))
+import importlib  # noqa: E402
+
+our_music = importlib.import_module("diffusion-piano_amd.music")  # only for the .mid parse, see docstring
 
 
 # --------------------------------------------------------------------------- stubs

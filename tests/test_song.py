@@ -1,0 +1,223 @@
+"""Native song ingestion (libpianosong.so, include/pianosong.h) against the Python
+restatement (oracle/music_ref.py, itself pinned to the reference's trajectory code through
+tests/golden/songs.json in test_golden.py, which now runs on the native path):
+
+* the three benchmark songs (+ fingering file): note sequences, trim, tables identical;
+* fuzzed Standard MIDI Files (several tracks, running status, tempo maps with same-tick
+  changes, overlapping / same-tick note on-off, velocity-0 offs, program changes, sysex,
+  sustain CCs): parse, trim and tables identical (times bit-equal), errors on the same
+  inputs;
+* annotation texts with comments, blank lines, malformed rows and out-of-range fingers;
+* malformed files raise ValueError; the library exports every declared symbol.
+"""
+import importlib
+import re
+import struct
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from helpers import DATA
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def mus():
+    return importlib.import_module("diffusion-piano_amd.music")
+
+
+@pytest.fixture(scope="module")
+def mref():
+    return importlib.import_module("music_ref")
+
+
+def notes_of(seq):
+    return [(n.pitch, n.start_time, n.end_time, n.velocity, n.part) for n in seq.notes]
+
+
+def ccs_of(seq):
+    return [(c.time, c.control_number, c.control_value) for c in seq.control_changes]
+
+
+def same_seq(a, b):
+    assert notes_of(a) == notes_of(b)
+    assert ccs_of(a) == ccs_of(b)
+    assert a.total_time == b.total_time
+
+
+def same_tables(a, b):
+    assert a.T == b.T and a.has_fingering == b.has_fingering
+    for x, y in ((a.goal, b.goal), (a.count, b.count), (a.keys, b.keys), (a.fingers, b.fingers)):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_song_library_exports_header_symbols():
+    lib = importlib.import_module("diffusion-piano_amd._lib")
+    L = lib.load_song()
+    header = (ROOT / "include" / "pianosong.h").read_text()
+    declared = set(re.findall(r"\b(pss_[a-z_]+)\s*\(", header))
+    assert declared == set(lib.SONG_EXPORTS)
+    assert L.pss_version() >= 1
+
+
+@pytest.mark.parametrize("name", ["Crossing Field Cut 10s.mid", "Guren no Yumiya Cut 14s.mid"])
+def test_fixture_songs_identical(mus, mref, name):
+    a, b = mus.parse_midi(DATA / name), mref.parse_midi(DATA / name)
+    same_seq(a, b)
+    if name.startswith("Guren"):
+        ann = DATA / "Guren no Yumiya Cut 14s_fingering v3.txt"
+        a = mus.add_fingering_from_annotation_file(DATA / name, ann)
+        b = mref.add_fingering_from_annotation_file(DATA / name, ann)
+        same_seq(a, b)
+        assert a.has_fingering()
+    a, b = mus.trim_silence(a), mref.trim_silence(b)
+    same_seq(a, b)
+    for dt, buf in ((0.05, 0.0), (0.05, 0.5), (0.01, 0.075), (0.02, 0.03)):
+        same_tables(mus.song_tables(a, dt, buf), mref.song_tables(b, dt, buf))
+
+
+# ------------------------------------------------------------------ fuzzed SMF files
+def varlen(v):
+    out = [v & 0x7F]
+    v >>= 7
+    while v:
+        out.append(0x80 | (v & 0x7F))
+        v >>= 7
+    return bytes(reversed(out))
+
+
+def random_smf(rng):
+    division = int(rng.choice([96, 220, 480, 960]))
+    ntr = int(rng.randint(1, 4))
+    chunks = []
+    for _ in range(ntr):
+        ev = bytearray()
+        last_status = None
+        open_pitches = []
+        for _ in range(int(rng.randint(5, 70))):
+            delta = int(rng.choice([0, 0, rng.randint(1, 40), rng.randint(40, 1500)]))
+            ev += varlen(delta)
+            r = rng.rand()
+            if r < 0.06:
+                ev += bytes([0xFF, 0x51, 3]) + int(rng.randint(250000, 1000000)).to_bytes(3, "big")
+                continue
+            if r < 0.08:
+                txt = bytes(rng.randint(32, 120, rng.randint(0, 6)).astype(np.uint8))
+                ev += bytes([0xFF, 0x01]) + varlen(len(txt)) + txt
+                continue
+            if r < 0.09:
+                ev += bytes([0xF0, 3, 0x7E, 0x01, 0xF7])
+                continue
+            ch = int(rng.choice([0, 0, 1, 9]))
+            if r < 0.13:
+                status, data = 0xC0 | ch, bytes([int(rng.randint(0, 128))])
+            elif r < 0.25:
+                status = 0xB0 | ch
+                data = bytes([int(rng.choice([64, 64, 7, 1])), int(rng.randint(0, 128))])
+            elif r < 0.6 or not open_pitches:
+                pitch = int(rng.randint(21, 109)) if rng.rand() < 0.98 else int(rng.randint(0, 128))
+                if open_pitches and rng.rand() < 0.3:
+                    pitch = int(rng.choice(open_pitches))  # re-strike of an open note
+                open_pitches.append(pitch)
+                status, data = 0x90 | ch, bytes([pitch, int(rng.randint(1, 128))])
+            else:
+                pitch = open_pitches.pop(int(rng.randint(len(open_pitches))))
+                if rng.rand() < 0.5:
+                    status, data = 0x90 | ch, bytes([pitch, 0])
+                else:
+                    status, data = 0x80 | ch, bytes([pitch, int(rng.randint(0, 128))])
+            if status == last_status and rng.rand() < 0.6:
+                ev += data  # running status
+            else:
+                ev += bytes([status]) + data
+            last_status = status
+        ev += bytes([0, 0xFF, 0x2F, 0])
+        chunks.append(b"MTrk" + struct.pack(">I", len(ev)) + bytes(ev))
+    return b"MThd" + struct.pack(">IHHH", 6, 1 if ntr > 1 else 0, ntr, division) + b"".join(chunks)
+
+
+def both(f, g):
+    """(result or the exception type) of the native call and of the restatement."""
+    out = []
+    for fn in (f, g):
+        try:
+            out.append(fn())
+        except (ValueError, IndexError, KeyError) as e:
+            out.append(type(e))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_fuzzed_smf(mus, mref, tmp_path, seed):
+    rng = np.random.RandomState(seed)
+    data = random_smf(rng)
+    path = tmp_path / f"f{seed}.mid"
+    path.write_bytes(data)
+    a, b = mus.parse_midi(path), mref.parse_midi(path)
+    same_seq(a, b)
+    assert a.notes or not b.notes
+    ta, tb = mus.trim_silence(a), mref.trim_silence(b)
+    same_seq(ta, tb)
+    for seq_a, seq_b in ((a, b), (ta, tb)):
+        dt = float(rng.choice([0.05, 0.02, 0.01]))
+        buf = float(rng.choice([0.0, 0.1, 0.025]))
+        ra, rb = both(lambda: mus.song_tables(seq_a, dt, buf), lambda: mref.song_tables(seq_b, dt, buf))
+        if isinstance(rb, type):
+            assert ra is ValueError and rb is ValueError, (ra, rb)
+        else:
+            same_tables(ra, rb)
+
+
+def test_fuzzed_annotations(mus, mref, tmp_path):
+    seq_path = DATA / "Guren no Yumiya Cut 14s.mid"
+    base = mref.parse_midi(seq_path)
+    rng = np.random.RandomState(4)
+    names = ["C", "C#", "Db", "D", "Eb", "E", "F", "F#", "G", "Ab", "A", "Bb", "B"]
+    for trial in range(20):
+        lines = ["// header", ""]
+        for n in rng.choice(len(base.notes), 40):
+            note = base.notes[n]
+            name = names[note.pitch % 12] + str(note.pitch // 12 - 1)
+            s = note.start_time + rng.uniform(-0.012, 0.012)
+            e = note.end_time + rng.uniform(-0.012, 0.012)
+            f = int(rng.randint(-1, 11))
+            row = [str(int(n)), f"{s:.6f}", f"{e:.6f}", name, "64", "80", "0", str(f)]
+            if rng.rand() < 0.05:
+                row = row[:7]  # malformed: 7 fields, skipped
+            lines.append("\t".join(row))
+        text = "\n".join(lines) + "\n"
+        ann = tmp_path / f"a{trial}.txt"
+        ann.write_text(text)
+        a = mus.add_fingering_from_annotation_file(seq_path, ann)
+        b = mref.add_fingering_from_annotation_file(seq_path, ann)
+        same_seq(a, b)
+    bad = tmp_path / "bad.txt"
+    bad.write_text("0\t1.0\t2.0\tH4\t64\t80\t0\t1\n")
+    with pytest.raises(ValueError):
+        mus.add_fingering_from_annotation_file(seq_path, bad)
+    with pytest.raises(ValueError):
+        mref.add_fingering_from_annotation_file(seq_path, bad)
+
+
+def test_malformed_files_raise(mus, tmp_path):
+    good = (DATA / "Crossing Field Cut 10s.mid").read_bytes()
+    cases = {"not_smf": b"RIFF" + good[4:], "truncated": good[:len(good) // 2],
+             "smpte": good[:12] + bytes([0xE7, 0x28]) + good[14:]}
+    for name, data in cases.items():
+        p = tmp_path / f"{name}.mid"
+        p.write_bytes(data)
+        with pytest.raises(ValueError):
+            mus.parse_midi(p)
+
+
+def test_parse_is_fast(mus):
+    """Init-time budget: the benchmark songs parse + trim + tabulate in well under a second."""
+    import time
+    t0 = time.perf_counter()
+    for _ in range(20):
+        seq = mus.add_fingering_from_annotation_file(DATA / "Guren no Yumiya Cut 14s.mid",
+                                                     DATA / "Guren no Yumiya Cut 14s_fingering v3.txt")
+        mus.song_tables(mus.trim_silence(seq), 0.05)
+    assert (time.perf_counter() - t0) / 20 < 0.05
