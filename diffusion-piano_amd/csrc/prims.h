@@ -122,6 +122,18 @@ __device__ __forceinline__ int small_excl_scan(int v, int lane, int* total) {
   return ex;
 }
 
+// Exchange point of a ONE-WAVE workgroup (every kernel here is launched with 64 threads):
+// the wave's LDS operations are performed in issue order, so a value another lane reads
+// after this point was written before it without any wait; what must not happen is the
+// compiler moving LDS accesses across it or keeping a stale LDS value in a register.
+// __syncthreads() would add s_waitcnt lgkmcnt(0), stalling on every LDS / scalar load in
+// flight at ~40 exchange points per physics substep.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct Contact {
   float pos[3], n[3], t1[3], t2[3], dist;
   int kind, key, g1, g2;  // g1: -1 for key/base (kind 0/1)
