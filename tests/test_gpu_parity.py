@@ -83,6 +83,31 @@ def test_teacher_forced_step(dp, ref, substep_only):
         assert med < 1e-5 and p99 < 5e-4, (med, p99, e.max())
 
 
+def test_teacher_forced_many_constraint_rows(dp, ref):
+    """States with m hand joints pushed past their limits (m = 4 .. 51), so the coupled
+    constraint rows span every Delassus path: one 16x16 MFMA tile (nrow <= 16), the three
+    tiles of nrow <= 32, and the lane-per-pair build above 32. One physics substep."""
+    n = 48
+    md, st, tc, g, o = _pair(dp, ref, "twinkle", n, control_timestep=0.005)
+    rng = np.random.RandomState(11)
+    q, v = random_states(md, n, rng, vscale=0.1)
+    q[:, :88] = np.clip(q[:, :88], 0.0, None)  # keys inside their range: hand limits dominate
+    for i in range(n):
+        for j in rng.choice(52, size=min(4 + i, 52), replace=False):
+            h, jj = divmod(int(j), 26)
+            lo, hi = md.dof_range[h][jj]
+            q[i, 88 + j] = lo - 0.01 if rng.rand() < 0.5 else hi + 0.01
+    s = dict(qpos=q, qvel=v, qacc_ws=np.zeros_like(q), ctrl=np.zeros((n, 44)), sustain=np.zeros(n),
+             t_idx=np.zeros(n, np.int32), last=np.zeros(n, np.uint8))
+    g.set_state(s)
+    o.set_state(s)
+    a = np.zeros((n, 45), np.float32)
+    g.step(torch.from_numpy(a).cuda())
+    o.step(a)
+    e = np.abs(_gstate(g)["qpos"] - o.get_state()["qpos"]).max(axis=1)
+    assert np.median(e) < 1e-6 and np.percentile(e, 90) < 5e-5, (np.median(e), np.percentile(e, 90), e.max())
+
+
 @pytest.mark.parametrize("name,kw", [("twinkle", {}), ("crossing_field", dict(trim_silence=True)),
                                      ("guren", dict(trim_silence=True))])
 def test_rewards_obs_and_step_types(dp, ref, name, kw):
