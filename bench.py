@@ -191,7 +191,7 @@ def main():
                          "bytes_per_env_step": bpe},
             "qpos_drift": drift_summary(),
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"] = cpu_baseline(dp, seq, task, args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(line), flush=True)
     env.close()
