@@ -45,6 +45,8 @@ struct ps_env {
   int *t_idx, *ncon;
   float *mus_acc, *mus_ep;  // MidiEvaluationWrapper: running sums of this episode, last episode
   int* mus_cnt;             // finished episodes per env
+  int* order;               // dispatch order of the step launch (longest-expected first)
+  bool ordered;
   uint8_t* last;
   bool applied_on;
 };
@@ -391,6 +393,7 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMalloc(&E->mus_acc, sizeof(float) * N * PS_NMUSIC));
   HIPCHK(hipMalloc(&E->mus_ep, sizeof(float) * N * PS_NMUSIC));
   HIPCHK(hipMalloc(&E->mus_cnt, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->order, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->last, N));
   HIPCHK(hipMemset(E->qpos, 0, sizeof(float) * N * NV));
   HIPCHK(hipMemset(E->qvel, 0, sizeof(float) * N * NV));
@@ -408,6 +411,7 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMemset(E->last, 0, N));
   HIPCHK(hipDeviceSynchronize());
   E->applied_on = false;
+  E->ordered = !(getenv("PIANOSIM_NO_ORDER") && atoi(getenv("PIANOSIM_NO_ORDER")));
   *out = E;
   return 0;
 }
@@ -418,8 +422,40 @@ void ps_destroy(ps_env* E) {
   hipFree(E->d_model); hipFree(E->d_goal); hipFree(E->d_count); hipFree(E->d_keys); hipFree(E->d_fingers);
   hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
-  hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt);
+  hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
   delete E;
+}
+
+// Dispatch order of a step launch: envs by their last contact count, descending, envs about
+// to auto-reset (no physics this step) last. Workgroups are dispatched in blockIdx order, so
+// the expensive envs start in the first wave of workgroups and the cheap ones fill the slots
+// freed late (longest-processing-time-first): the launch's tail is shorter. Each env's
+// result is independent of the order.
+constexpr int ORDER_THREADS = 1024;
+__global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restrict__ ncon,
+                                                              const uint8_t* __restrict__ last,
+                                                              int* __restrict__ order, int n) {
+  constexpr int NB = MAXCON + 2;  // bucket 0: resets, 1 + c: c contacts
+  __shared__ int hist[NB], base[NB];
+  if (threadIdx.x < NB) hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int b = last[e] ? 0 : 1 + min(max(ncon[e], 0), MAXCON);
+    atomicAdd(&hist[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = NB - 1; b >= 0; b--) {  // most contacts first, resets last
+      base[b] = acc;
+      acc += hist[b];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int b = last[e] ? 0 : 1 + min(max(ncon[e], 0), MAXCON);
+    order[atomicAdd(&base[b], 1)] = e;
+  }
 }
 
 static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask, float* obs, float* reward,
@@ -431,8 +467,15 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
   if (const char* sk = getenv("PIANOSIM_SKIP")) cfg.skip = atoi(sk);
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt};
+  const int* order = nullptr;
+  if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
+    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->ncon, E->last, E->order,
+                       E->n);
+    HIPCHK(hipGetLastError());
+    order = E->order;
+  }
   hipLaunchKernelGGL(pianosim_kernel, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b, action,
-                     mask, obs, reward, discount, step_type, mode, E->n);
+                     mask, obs, reward, discount, step_type, mode, E->n, order);
   HIPCHK(hipGetLastError());
   return 0;
 }
