@@ -532,8 +532,11 @@ class PPOAgent:
         if self._wandb is not None:
             for rec in log.cpu().numpy():
                 self._wandb.log(dict(zip(LOG_KEYS, map(float, rec))))
-        mean_reward = r.mean().item()
-        mean_critic_loss = float(log[-1, 1])
+        stats = torch.stack([r.mean(), log[-1, 1]])
+        if self.distributed:  # one plateau decision for all replicas (else their lrs drift apart)
+            torch.distributed.all_reduce(stats, group=self.process_group)
+            stats /= torch.distributed.get_world_size(self.process_group)
+        mean_reward, mean_critic_loss = (float(x) for x in stats.cpu())
         self.actor_scheduler.step(mean_reward)
         self.critic_scheduler.step(mean_critic_loss)
         self.timing["update_s"] = time.perf_counter() - t0
