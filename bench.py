@@ -97,6 +97,15 @@ def pmc_traffic(n_envs, song):
     return None
 
 
+def issue_summary(n_envs, song):
+    """Where the wave time goes (the binding limit: latency, not HBM), from the committed SQ
+    counter pass (tools/collect_pmc.py): fractions of the waves' lifetime issuing / waiting."""
+    d = _profile("pmc_latest.json")
+    if d and d.get("envs") == n_envs and d.get("song", song) == song and "wave_issue_frac" in d:
+        return {k: d[k] for k in ("wave_issue_frac", "wave_wait_frac", "wave_ifetch_frac", "valu_insts_per_env_step")}
+    return None
+
+
 def drift_summary():
     """qpos L-inf drift vs the fp64 CPU step, from the committed drift report written by
     tests/test_gpu_drift.py (PIANOSIM_REPORT=profiles/drift_latest.json)."""
@@ -188,7 +197,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
-                         "bytes_per_env_step": bpe},
+                         "kernel_ms_note": "HIP events around ps_step: order_kernel (counting sort, ~5 us) + pianosim_kernel",
+                         "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song)},
             "qpos_drift": drift_summary(),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure

@@ -1,9 +1,11 @@
 """Summarise rocprofv3 outputs for pianosim_kernel into profiles/.
 
-usage: python tools/collect_pmc.py <trace_dir> <fetch_dir> <write_dir> <envs> <song> <out_prefix> [warmup]
+usage: python tools/collect_pmc.py <trace_dir> <fetch_dir> <write_dir> <envs> <song> <out_prefix> [warmup] [sq_dir]
 
 * <trace_dir>: `rocprofv3 --kernel-trace --stats --output-format csv` of bench.py
 * <fetch_dir>/<write_dir>: separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes
+* [sq_dir]: a `--pmc` pass of the SQ wave-state counters (SQ_COUNTERS below): how much of
+  the waves' lifetime issues an instruction vs waits on a counter / instruction fetch
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md, HBM:
 FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950; units KB).
 """
@@ -34,9 +36,14 @@ def counter(d, name):
     return sum(vals) / len(vals) if vals else None
 
 
+SQ_COUNTERS = ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY",
+               "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_LDS")
+
+
 def main():
     tdir, fdir, wdir, envs, song, prefix = sys.argv[1:4] + [int(sys.argv[4])] + sys.argv[5:7]
     warmup = int(sys.argv[7]) if len(sys.argv) > 7 else 5
+    sqdir = sys.argv[8] if len(sys.argv) > 8 else None
     stats = [r for r in rows(tdir, "*kernel_stats.csv") if "pianosim_kernel" in r.get("Name", "")]
     fetch_kb = counter(fdir, "FETCH_SIZE")
     write_kb = counter(wdir, "WRITE_SIZE")
@@ -56,6 +63,15 @@ def main():
         out["fetch_kb_per_launch"] = fetch_kb
         out["write_kb_per_launch"] = write_kb
         out["hbm_bytes_per_launch"] = (2.0 * fetch_kb + write_kb) * 1024.0
+    if sqdir:
+        sq = {c: counter(sqdir, c) for c in SQ_COUNTERS}
+        if all(v is not None for v in sq.values()):
+            out["sq_per_launch"] = sq
+            wc = sq["SQ_WAVE_CYCLES"]
+            out["wave_issue_frac"] = sq["SQ_ACTIVE_INST_ANY"] / wc  # lifetime issuing
+            out["wave_wait_frac"] = sq["SQ_WAIT_ANY"] / wc  # waiting on s_waitcnt
+            out["wave_ifetch_frac"] = sq["SQ_WAIT_INST_ANY"] / wc  # waiting on instruction fetch
+            out["valu_insts_per_env_step"] = sq["SQ_INSTS_VALU"] / envs
     Path("profiles").mkdir(exist_ok=True)
     if stats:
         with open(f"profiles/{prefix}_kernel_stats.csv", "w", newline="") as fh:

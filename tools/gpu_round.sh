@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 P=${1:-r01}
 SONG=crossing_field
 mkdir -p gpurun_out profiles
-rm -rf gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write
+rm -rf gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write gpurun_out/${P}_sq
 PIANOSIM_REPORT=profiles/${P}_drift.json timeout -k 10 500 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1
 RC=$?
 echo "PYTEST_EXIT $RC" >> gpurun_out/pytest_gpu.log
@@ -17,7 +17,8 @@ cp profiles/${P}_drift.json profiles/drift_latest.json 2>/dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${P}_trace -- python bench.py --no-cpu-baseline --steps 20 > gpurun_out/${P}_trace.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${P}_fetch -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/${P}_fetch.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${P}_write -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/${P}_write.log 2>&1 || exit 4
-python tools/collect_pmc.py gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write 4096 $SONG $P > gpurun_out/pmc.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d gpurun_out/${P}_sq -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/${P}_sq.log 2>&1 || exit 7
+python tools/collect_pmc.py gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write 4096 $SONG $P 5 gpurun_out/${P}_sq > gpurun_out/pmc.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
 cp gpurun_out/bench.json profiles/${P}_bench.json
 # per-phase cycle split from the -DPS_TIMING build (built on the CPU side beforehand)
