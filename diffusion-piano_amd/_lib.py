@@ -20,7 +20,8 @@ EXPORTS = (
 
 # Every entry point declared in include/pianorl.h.
 RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample",
-              "prl_clip_adam")
+              "prl_clip_adam", "prl_gather_minibatch", "prl_lnrelu_fwd", "prl_lnrelu_bwd", "prl_actor_head",
+              "prl_critic_head", "prl_colsums")
 
 _lib = None
 _rl = None
@@ -85,6 +86,12 @@ def load_rl() -> C.CDLL:
     L.prl_normalize.argtypes = [vp, i32, f32, vp]
     L.prl_gauss_sample.argtypes = [vp, vp, i32, i32, u64, u64, vp, vp, vp]
     L.prl_clip_adam.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_int64), i32, vp, vp, f32, f32, f32, f32, vp, vp]
+    L.prl_gather_minibatch.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.prl_lnrelu_fwd.argtypes = [vp, vp, vp, vp, i32, i32, f32, f32, u64, vp, i32, vp, vp, vp, vp]
+    L.prl_lnrelu_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, u64, vp, i32, vp, vp, vp, vp]
+    L.prl_actor_head.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, vp, vp, vp, vp, vp]
+    L.prl_critic_head.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
+    L.prl_colsums.argtypes = [i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(f32), C.POINTER(vp), i32, vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
     _rl = L

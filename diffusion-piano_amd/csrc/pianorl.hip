@@ -290,6 +290,189 @@ __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restri
   }
 }
 
+
+// ---------------------------------------------------------------- fused minibatch step
+// The PPO minibatch step of ppo_v2.py:266-293 with the backward pass written out: the GEMMs
+// stay library GEMMs (hipBLASLt, issued by ppo.py), everything between them is one kernel
+// per layer and direction instead of torch's ~8 elementwise / reduction launches.
+
+// dropout keep decision: Philox4x32-10 keyed by (seed, step counter), counter (col, row, layer)
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t step, int layer, int row, int col, float p) {
+  uint32_t c[4] = {(uint32_t)col, (uint32_t)row, (uint32_t)step ^ ((uint32_t)layer << 24), (uint32_t)(step >> 32)};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (float)c[0] * 2.3283064e-10f >= p;
+}
+
+// block sum over the row's H <= 1024 threads (fp32), result broadcast
+__device__ __forceinline__ float row_sum(float v, float* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; i++) s += red[i];
+  return s;
+}
+
+// gather the minibatch rows (DataLoader batch, ppo_v2.py:266-271); thread 0 of block 0 also
+// advances the dropout step counter of this minibatch
+__global__ void gather_kernel(const float* __restrict__ S, int sdim, const float* __restrict__ A, int adim,
+                              const float* __restrict__ lp, const float* __restrict__ adv, const float* __restrict__ ret,
+                              const int64_t* __restrict__ idx, int B, float* __restrict__ oS, float* __restrict__ oA,
+                              float* __restrict__ olp, float* __restrict__ oadv, float* __restrict__ oret,
+                              uint64_t* __restrict__ step) {
+  const int r = blockIdx.x;
+  if (r == 0 && threadIdx.x == 0 && step) *step += 1;
+  if (r >= B) return;
+  const int64_t src = idx[r];
+  for (int i = threadIdx.x; i < sdim; i += blockDim.x) oS[(size_t)r * sdim + i] = S[(size_t)src * sdim + i];
+  for (int i = threadIdx.x; i < adim; i += blockDim.x) oA[(size_t)r * adim + i] = A[(size_t)src * adim + i];
+  if (threadIdx.x == 0) {
+    olp[r] = lp[src];
+    oadv[r] = adv[src];
+    oret[r] = ret[src];
+  }
+}
+
+// y = dropout(LayerNorm(relu(z + b))) of one row per block (nn.ReLU, nn.LayerNorm eps,
+// biased variance; nn.Dropout(p) in train mode); keeps xhat and 1/std for the backward
+__global__ void lnrelu_fwd_kernel(const float* __restrict__ Z, const float* __restrict__ bias,
+                                  const float* __restrict__ gamma, const float* __restrict__ beta, int H, float eps,
+                                  float p, uint64_t seed, const uint64_t* __restrict__ step, int layer,
+                                  float* __restrict__ Y, float* __restrict__ xhat, float* __restrict__ rstd) {
+  __shared__ float red[16];
+  const int r = blockIdx.x, c = threadIdx.x;
+  const float x = c < H ? fmaxf(Z[(size_t)r * H + c] + bias[c], 0.f) : 0.f;
+  const float mean = row_sum(x, red) / (float)H;
+  const float d = c < H ? x - mean : 0.f;
+  const float var = row_sum(d * d, red) / (float)H;
+  const float rs = 1.f / sqrtf(var + eps);
+  if (c < H) {
+    const float xh = d * rs;
+    float y = xh * gamma[c] + beta[c];
+    if (p > 0.f) y = keep_elem(seed, *step, layer, r, c, p) ? y / (1.f - p) : 0.f;
+    Y[(size_t)r * H + c] = y;
+    xhat[(size_t)r * H + c] = xh;
+  }
+  if (c == 0) rstd[r] = rs;
+}
+
+// backward of lnrelu_fwd for one row per block: dZ, and the per-row terms whose column sums
+// are the gamma / beta gradients (dye = the gradient reaching the LayerNorm output)
+__global__ void lnrelu_bwd_kernel(const float* __restrict__ dY, const float* __restrict__ Z,
+                                  const float* __restrict__ bias, const float* __restrict__ xhat,
+                                  const float* __restrict__ rstd, const float* __restrict__ gamma, int H, float p,
+                                  uint64_t seed, const uint64_t* __restrict__ step, int layer, float* __restrict__ dZ,
+                                  float* __restrict__ dyx, float* __restrict__ dye) {
+  __shared__ float red[16];
+  const int r = blockIdx.x, c = threadIdx.x;
+  float g = 0.f, xh = 0.f;
+  if (c < H) {
+    g = dY[(size_t)r * H + c];
+    if (p > 0.f) g = keep_elem(seed, *step, layer, r, c, p) ? g / (1.f - p) : 0.f;
+    xh = xhat[(size_t)r * H + c];
+  }
+  const float dxh = g * (c < H ? gamma[c] : 0.f);
+  const float m1 = row_sum(dxh, red) / (float)H;
+  const float m2 = row_sum(dxh * xh, red) / (float)H;
+  if (c < H) {
+    const float dr = rstd[r] * (dxh - m1 - xh * m2);
+    dZ[(size_t)r * H + c] = Z[(size_t)r * H + c] + bias[c] > 0.f ? dr : 0.f;
+    dyx[(size_t)r * H + c] = g * xh;
+    dye[(size_t)r * H + c] = g;
+  }
+}
+
+// actor head + clipped surrogate (ppo_v2.py:70-74, 272-279), one wave per row (A <= 64):
+// mu = tanh(z + b), log-prob of the batch action, ratio, the loss row and its gradients
+// dZ (d loss / d z) and the per-row log_std gradient; torch.minimum splits the gradient
+// evenly on a tie and clamp passes it at the bounds (derivatives.yaml)
+__global__ void actor_head_kernel(const float* __restrict__ Z, const float* __restrict__ bias,
+                                  const float* __restrict__ log_std, const float* __restrict__ act,
+                                  const float* __restrict__ old_lp, const float* __restrict__ adv, int B, int A,
+                                  float clip, float ent_coef, float* __restrict__ dZ, float* __restrict__ dls,
+                                  float* __restrict__ stats, float* __restrict__ ent_rows) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float mu = 0.f, sd = 1.f, ls = 0.f, a = 0.f, lp = 0.f;
+  bool inr = false;
+  if (lane < A) {
+    mu = tanhf(Z[(size_t)r * A + lane] + bias[lane]);
+    const float l = log_std[lane];
+    inr = l >= -20.f && l <= 2.f;
+    ls = fminf(fmaxf(l, -20.f), 2.f);
+    sd = expf(ls);
+    a = act[(size_t)r * A + lane];
+    const float dx = a - mu;
+    lp = -(dx * dx) / (2.f * sd * sd) - ls - 0.91893853f;
+  }
+  // Normal entropy mean over the action dims (dist.entropy().mean(): the same for every row)
+  float ent = lane < A ? 0.5f + 0.91893853f + ls : 0.f;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lp += __shfl_xor(lp, off, 64);
+    ent += __shfl_xor(ent, off, 64);
+  }
+  ent /= (float)A;
+  const float ratio = expf(lp - old_lp[r]);
+  const float A_ = adv[r];
+  const float rc = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip);
+  const float s1 = ratio * A_, s2 = rc * A_;
+  const float w1 = s1 < s2 ? 1.f : (s1 == s2 ? 0.5f : 0.f);
+  const float w2 = 1.f - w1;
+  const float inclip = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+  // loss = -mean(min(s1, s2)) - ent_coef * entropy: d loss / d ratio for this row
+  const float g = -(w1 * A_ + w2 * A_ * inclip) / (float)B;
+  const float gl = g * ratio;  // d loss / d log-prob
+  if (lane < A) {
+    const float dx = a - mu, iv = 1.f / (sd * sd);
+    dZ[(size_t)r * A + lane] = gl * dx * iv * (1.f - mu * mu);
+    // log-prob term (a - mu)^2 / sd^2 - 1, and the entropy bonus -ent_coef / A spread over rows
+    dls[(size_t)r * A + lane] = inr ? gl * (dx * dx * iv - 1.f) - ent_coef / ((float)A * (float)B) : 0.f;
+  }
+  if (lane == 0) {
+    stats[r] = -fminf(s1, s2) - ent_coef * ent;  // row of the actor loss (its mean is the loss)
+    ent_rows[r] = ent;
+  }
+}
+
+// critic head + MSE (ppo_v2.py:283-284): v = z + c, loss row (v - ret)^2, d loss / d z
+__global__ void critic_head_kernel(const float* __restrict__ Z, const float* __restrict__ bias,
+                                   const float* __restrict__ ret, int B, float* __restrict__ dZ, float* __restrict__ v_out,
+                                   float* __restrict__ sq) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  const float v = Z[r] + bias[0];
+  const float e = v - ret[r];
+  dZ[r] = 2.f * e / (float)B;
+  v_out[r] = v;
+  sq[r] = e * e;
+}
+
+// column sums of several [B, C_i] arrays in one launch (deterministic: one thread per column
+// walks the rows in order); out_i[c] = scale_i * sum_r X_i[r][c]
+struct ColSums {
+  const float* src[PRL_MAX_COLSUMS];
+  float* dst[PRL_MAX_COLSUMS];
+  int cols[PRL_MAX_COLSUMS];
+  float scale[PRL_MAX_COLSUMS];
+  int n, B;
+};
+__global__ void colsums_kernel(ColSums cs) {
+  const int i = blockIdx.y;
+  if (i >= cs.n) return;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int C = cs.cols[i];
+  if (c >= C) return;
+  const float* x = cs.src[i];
+  float acc = 0.f;
+  for (int r = 0; r < cs.B; r++) acc += x[(size_t)r * C + c];
+  cs.dst[i][c] = acc * cs.scale[i];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI
@@ -355,6 +538,81 @@ int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_av
   const int blocks = (int)std::min<int64_t>(1024, (n + ADAM_THREADS * 4 - 1) / (ADAM_THREADS * 4));
   clip_adam_kernel<<<blocks, ADAM_THREADS, 0, (hipStream_t)stream>>>(param, grad, exp_avg, exp_avg_sq, sg, scratch, lr,
                                                                     step, beta1, beta2, eps, max_norm, parts);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_gather_minibatch(const float* S, int sdim, const float* A, int adim, const float* lp, const float* adv,
+                         const float* ret, const int64_t* idx, int B, float* oS, float* oA, float* olp, float* oadv,
+                         float* oret, uint64_t* dropout_step, void* stream) {
+  if (!S || !A || !lp || !adv || !ret || !idx || !oS || !oA || !olp || !oadv || !oret) return fail("prl_gather_minibatch: null");
+  if (B <= 0 || sdim <= 0 || adim <= 0) return fail("prl_gather_minibatch: bad sizes");
+  gather_kernel<<<B, 256, 0, (hipStream_t)stream>>>(S, sdim, A, adim, lp, adv, ret, idx, B, oS, oA, olp, oadv, oret,
+                                                    dropout_step);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_lnrelu_fwd(const float* Z, const float* bias, const float* gamma, const float* beta, int B, int H, float eps,
+                   float p, uint64_t seed, const uint64_t* dropout_step, int layer, float* Y, float* xhat, float* rstd,
+                   void* stream) {
+  if (!Z || !bias || !gamma || !beta || !Y || !xhat || !rstd) return fail("prl_lnrelu_fwd: null");
+  if (B <= 0 || H <= 0 || H > 1024 || (p > 0.f && !dropout_step)) return fail("prl_lnrelu_fwd: bad arguments");
+  const int threads = (H + 63) / 64 * 64;
+  lnrelu_fwd_kernel<<<B, threads, 0, (hipStream_t)stream>>>(Z, bias, gamma, beta, H, eps, p, seed, dropout_step, layer,
+                                                            Y, xhat, rstd);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_lnrelu_bwd(const float* dY, const float* Z, const float* bias, const float* xhat, const float* rstd,
+                   const float* gamma, int B, int H, float p, uint64_t seed, const uint64_t* dropout_step, int layer,
+                   float* dZ, float* dyx, float* dye, void* stream) {
+  if (!dY || !Z || !bias || !xhat || !rstd || !gamma || !dZ || !dyx || !dye) return fail("prl_lnrelu_bwd: null");
+  if (B <= 0 || H <= 0 || H > 1024 || (p > 0.f && !dropout_step)) return fail("prl_lnrelu_bwd: bad arguments");
+  const int threads = (H + 63) / 64 * 64;
+  lnrelu_bwd_kernel<<<B, threads, 0, (hipStream_t)stream>>>(dY, Z, bias, xhat, rstd, gamma, H, p, seed, dropout_step,
+                                                            layer, dZ, dyx, dye);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_actor_head(const float* Z, const float* bias, const float* log_std, const float* act, const float* old_lp,
+                   const float* adv, int B, int A, float clip, float ent_coef, float* dZ, float* dls, float* stats,
+                   float* ent_rows, void* stream) {
+  if (!Z || !bias || !log_std || !act || !old_lp || !adv || !dZ || !dls || !stats || !ent_rows)
+    return fail("prl_actor_head: null");
+  if (B <= 0 || A <= 0 || A > 64) return fail("prl_actor_head: need 0 < A <= 64");
+  actor_head_kernel<<<(B + 3) / 4, 256, 0, (hipStream_t)stream>>>(Z, bias, log_std, act, old_lp, adv, B, A, clip,
+                                                                  ent_coef, dZ, dls, stats, ent_rows);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_critic_head(const float* Z, const float* bias, const float* ret, int B, float* dZ, float* v, float* sq,
+                    void* stream) {
+  if (!Z || !bias || !ret || !dZ || !v || !sq || B <= 0) return fail("prl_critic_head: bad arguments");
+  critic_head_kernel<<<(B + 255) / 256, 256, 0, (hipStream_t)stream>>>(Z, bias, ret, B, dZ, v, sq);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int prl_colsums(int n, const float* const* src, const int* cols, const float* scale, float* const* dst, int B,
+                void* stream) {
+  if (n <= 0 || n > PRL_MAX_COLSUMS || !src || !cols || !dst || B <= 0) return fail("prl_colsums: bad arguments");
+  ColSums cs{};
+  int cmax = 0;
+  for (int i = 0; i < n; i++) {
+    if (!src[i] || !dst[i] || cols[i] <= 0) return fail("prl_colsums: bad entry");
+    cs.src[i] = src[i];
+    cs.dst[i] = dst[i];
+    cs.cols[i] = cols[i];
+    cs.scale[i] = scale ? scale[i] : 1.f;
+    cmax = cols[i] > cmax ? cols[i] : cmax;
+  }
+  cs.n = n;
+  cs.B = B;
+  colsums_kernel<<<dim3((cmax + 127) / 128, n), 128, 0, (hipStream_t)stream>>>(cs);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -303,12 +303,125 @@ class FlatAdam(GradBucket):
             float(self.eps), float(self.max_norm), self.scratch.data_ptr(), _stream()))
 
 
+# ---------------------------------------------------------------- fused minibatch step
+class FusedStep:
+    """The minibatch step of ppo_v2.py:266-293 (actor and critic forward, losses, backward)
+    without autograd: the 8 + 8 GEMMs per network go to hipBLASLt through ``torch.mm``
+    (gradient GEMMs written straight into the flat gradient bucket), every op between them
+    is ONE libpianorl kernel per layer and direction (bias + ReLU + LayerNorm (+ Dropout)
+    forward / backward, the Gaussian-policy surrogate head, the MSE head), and all bias /
+    LayerNorm / log_std gradients and the logged means come out of one column-sum launch:
+    ~40 launches instead of the ~150 of torch autograd. Numerically the same math as the
+    autograd path (tests/test_gpu_ppo.py compares them)."""
+
+    def __init__(self, agent: "PPOAgent"):
+        self.agent = agent
+        a, c = agent.actor.network, agent.critic.network
+        # (linear, layernorm, dropout p) per hidden layer, then the output linear
+        self.actor = [(a[0], a[2], 0.0), (a[3], a[5], 0.0), (a[6], a[8], 0.0)], a[9]
+        self.critic = [(c[0], c[2], 0.1), (c[4], c[6], 0.1), (c[8], c[10], 0.0)], c[11]
+        self.step = torch.zeros(1, dtype=torch.int64, device=agent.device)  # dropout draw counter
+        self.seed = agent._seed ^ 0x2545F4914F6CDD1D
+        self.bufs = {}
+
+    def _buffers(self, B):
+        if B in self.bufs:
+            return self.bufs[B]
+        ag = self.agent
+        f32 = dict(device=ag.device, dtype=torch.float32)
+        sdim, adim = ag._S.shape[1], ag._A.shape[1]
+        b = dict(S=torch.empty(B, sdim, **f32), A=torch.empty(B, adim, **f32), LP=torch.empty(B, **f32),
+                 ADV=torch.empty(B, **f32), RET=torch.empty(B, **f32))
+        for net, (hidden, out) in (("a", self.actor), ("c", self.critic)):
+            for i, (lin, ln, p) in enumerate(hidden):
+                H = lin.out_features
+                for k in ("Z", "Y", "XH", "dY", "dZ", "dyx", "dye"):
+                    b[f"{net}{k}{i}"] = torch.empty(B, H, **f32)
+                b[f"{net}rs{i}"] = torch.empty(B, **f32)
+            b[f"{net}Zo"] = torch.empty(B, out.out_features, **f32)
+            b[f"{net}dZo"] = torch.empty(B, out.out_features, **f32)
+        b["dls"] = torch.empty(B, adim, **f32)
+        for k in ("arow", "ent", "v", "sq"):
+            b[k] = torch.empty(B, **f32)
+        # one column-sum launch: every bias / LayerNorm / log_std gradient + the logged means
+        # (actor loss, critic loss, entropy, value, return, advantage -> agent._log_row)
+        L = ag._log_row
+        entries = []
+        for net, (hidden, out) in (("a", self.actor), ("c", self.critic)):
+            for i, (lin, ln, p) in enumerate(hidden):
+                H = lin.out_features
+                entries += [(b[f"{net}dZ{i}"], H, 1.0, lin.bias.grad), (b[f"{net}dyx{i}"], H, 1.0, ln.weight.grad),
+                            (b[f"{net}dye{i}"], H, 1.0, ln.bias.grad)]
+            entries.append((b[f"{net}dZo"], out.out_features, 1.0, out.bias.grad))
+        entries.append((b["dls"], adim, 1.0, ag.actor.log_std.grad))
+        for j, k in enumerate(("arow", "sq", "ent", "v", "RET", "ADV")):
+            entries.append((b[k], 1, 1.0 / B, L[j:j + 1]))
+        n = len(entries)
+        b["_cs"] = ((C.c_void_p * n)(*[e[0].data_ptr() for e in entries]), (C.c_int * n)(*[e[1] for e in entries]),
+                    (C.c_float * n)(*[e[2] for e in entries]), (C.c_void_p * n)(*[e[3].data_ptr() for e in entries]), n)
+        self.bufs[B] = b
+        return b
+
+    def __call__(self, idx):
+        with torch.no_grad():  # the backward is written out: no autograd graph
+            self._step(idx)
+
+    def _step(self, idx):
+        ag, R, st = self.agent, _lib.load_rl(), _stream()
+        B = idx.numel()
+        b = self._buffers(B)
+        sdim, adim = ag._S.shape[1], ag._A.shape[1]
+        chk = _lib.check_rl
+        train = ag.critic.training
+        chk(R.prl_gather_minibatch(ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(), ag._ADV.data_ptr(),
+                                   ag._RET.data_ptr(), idx.data_ptr(), B, b["S"].data_ptr(), b["A"].data_ptr(),
+                                   b["LP"].data_ptr(), b["ADV"].data_ptr(), b["RET"].data_ptr(), self.step.data_ptr(), st))
+        for net, (hidden, out) in (("a", self.actor), ("c", self.critic)):
+            x = b["S"]
+            for i, (lin, ln, p) in enumerate(hidden):  # forward
+                p = p if (net == "a" or train) else 0.0
+                Z = b[f"{net}Z{i}"]
+                torch.mm(x, lin.weight.t(), out=Z)
+                chk(R.prl_lnrelu_fwd(Z.data_ptr(), lin.bias.data_ptr(), ln.weight.data_ptr(), ln.bias.data_ptr(), B,
+                                     lin.out_features, float(ln.eps), float(p), self.seed, self.step.data_ptr(), i,
+                                     b[f"{net}Y{i}"].data_ptr(), b[f"{net}XH{i}"].data_ptr(),
+                                     b[f"{net}rs{i}"].data_ptr(), st))
+                x = b[f"{net}Y{i}"]
+            torch.mm(x, out.weight.t(), out=b[f"{net}Zo"])
+            if net == "a":
+                chk(R.prl_actor_head(b["aZo"].data_ptr(), out.bias.data_ptr(), ag.actor.log_std.data_ptr(),
+                                     b["A"].data_ptr(), b["LP"].data_ptr(), b["ADV"].data_ptr(), B, adim,
+                                     float(ag.epsilon), float(ag.entropy_coef), b["adZo"].data_ptr(), b["dls"].data_ptr(),
+                                     b["arow"].data_ptr(), b["ent"].data_ptr(), st))
+            else:
+                chk(R.prl_critic_head(b["cZo"].data_ptr(), out.bias.data_ptr(), b["RET"].data_ptr(), B,
+                                      b["cdZo"].data_ptr(), b["v"].data_ptr(), b["sq"].data_ptr(), st))
+            dz = b[f"{net}dZo"]  # backward
+            torch.mm(dz.t(), x, out=out.weight.grad)
+            dy = torch.mm(dz, out.weight, out=b[f"{net}dY{len(hidden) - 1}"])
+            for i in reversed(range(len(hidden))):
+                lin, ln, p = hidden[i]
+                p = p if (net == "a" or train) else 0.0
+                chk(R.prl_lnrelu_bwd(dy.data_ptr(), b[f"{net}Z{i}"].data_ptr(), lin.bias.data_ptr(),
+                                     b[f"{net}XH{i}"].data_ptr(), b[f"{net}rs{i}"].data_ptr(), ln.weight.data_ptr(), B,
+                                     lin.out_features, float(p), self.seed, self.step.data_ptr(), i,
+                                     b[f"{net}dZ{i}"].data_ptr(), b[f"{net}dyx{i}"].data_ptr(),
+                                     b[f"{net}dye{i}"].data_ptr(), st))
+                dz = b[f"{net}dZ{i}"]
+                xin = b["S"] if i == 0 else b[f"{net}Y{i - 1}"]
+                torch.mm(dz.t(), xin, out=lin.weight.grad)
+                if i > 0:
+                    dy = torch.mm(dz, lin.weight, out=b[f"{net}dY{i - 1}"])
+        src, cols, scale, dst, n = b["_cs"]
+        chk(R.prl_colsums(n, src, cols, scale, dst, B, st))
+
+
 # ---------------------------------------------------------------- the agent (ppo_v2.py:133-336)
 class PPOAgent:
     def __init__(self, state_dim, action_dim, lr=1e-4, gamma=0.99, epsilon=0.2, entropy_coef=0.01, value_coef=1.0,
                  max_grad_norm=0.5, ppo_epochs=10, batch_size=64, device="cuda", checkpoint_dir="checkpoints",
                  use_wandb=True, *, gae_lambda=0.95, process_group=None, graphs=True, sample_seed=None,
-                 tune_gemms=False):
+                 tune_gemms=False, fused=True):
         if not torch.cuda.is_available():
             raise _lib.PianosimError("PPOAgent needs a ROCm GPU (torch.cuda.is_available() is False)")
         _lib.load_rl()  # fail loudly if the kernels are missing
@@ -374,6 +487,8 @@ class PPOAgent:
         self._cap_stream = torch.cuda.Stream(self.device)
         self.last_update_log = None
         self.timing = {}
+        self.fused = fused
+        self._fused = None
 
     # -- acting (ppo_v2.py:211-218)
     def select_actions(self, states):
@@ -389,6 +504,13 @@ class PPOAgent:
 
     # -- minibatch step (ppo_v2.py:266-293): forward + both backwards | all-reduce | clip + steps
     def _forward_backward(self, idx, log_row):
+        if self.fused:
+            if self._fused is None:
+                self._fused = FusedStep(self)
+            self._fused(idx)  # writes self._log_row
+            if log_row.data_ptr() != self._log_row.data_ptr():
+                log_row.copy_(self._log_row)
+            return
         b_s = self._S.index_select(0, idx)
         b_a = self._A.index_select(0, idx)
         b_lp = self._LP.index_select(0, idx)
@@ -468,6 +590,7 @@ class PPOAgent:
         self._idx = torch.zeros(self.batch_size, device=self.device, dtype=torch.int64)
         self._log_row = torch.zeros(len(LOG_KEYS), **f32)
         self._graph = None  # buffers moved: re-capture
+        self._fused = None
         self._graph_eager_left = 2
 
     def _prepare(self, states, actions, rewards, log_probs, next_states, dones):

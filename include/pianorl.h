@@ -18,6 +18,9 @@
  *                        unbiased std as torch.std.
  *   prl_clip_adam     <- clip_grad_norm_(max_grad_norm) + optimizer.step() of each network
  *                        (ppo_v2.py:280-293), fused over one flat parameter buffer.
+ *   prl_gather_minibatch, prl_lnrelu_fwd / _bwd, prl_actor_head, prl_critic_head,
+ *   prl_colsums       <- the minibatch step's forward + autograd backward (ppo_v2.py:266-293)
+ *                        between the GEMMs: one launch per layer and direction.
  *   prl_gauss_sample  <- select_actions: Normal(mean, exp(clamp(log_std,-20,2))).sample() and
  *                        log_prob(actions).sum(1) (ppo_v2.py:70-74, 211-218). Counter-based
  *                        Philox4x32-10 keyed by (seed, offset, row, column).
@@ -68,6 +71,45 @@ int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint
 int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
                   int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
                   double* scratch, void* stream);
+
+/* ---- fused minibatch step (ppo_v2.py:266-293 with the backward written out; the GEMMs
+ * between these are library GEMMs). All row-major fp32 [rows, cols]. */
+#define PRL_MAX_COLSUMS 32
+
+/* gather minibatch rows idx[B] (int64) of S [N, sdim], A [N, adim], lp/adv/ret [N]; also
+ * increments *dropout_step (device u64, may be NULL): one dropout draw per minibatch */
+int prl_gather_minibatch(const float* S, int sdim, const float* A, int adim, const float* lp, const float* adv,
+                         const float* ret, const int64_t* idx, int B, float* oS, float* oA, float* olp, float* oadv,
+                         float* oret, uint64_t* dropout_step, void* stream);
+
+/* Y = Dropout_p(LayerNorm(ReLU(Z + bias))) per row (H <= 1024); xhat, rstd kept for the
+ * backward. p = 0: no dropout. Keep mask: Philox(seed, *dropout_step, layer, row, col). */
+int prl_lnrelu_fwd(const float* Z, const float* bias, const float* gamma, const float* beta, int B, int H, float eps,
+                   float p, uint64_t seed, const uint64_t* dropout_step, int layer, float* Y, float* xhat, float* rstd,
+                   void* stream);
+
+/* backward: dZ [B, H]; dyx = dY' * xhat and dye = dY' (dY' = dY through the dropout mask),
+ * whose column sums are the LayerNorm gamma / beta gradients */
+int prl_lnrelu_bwd(const float* dY, const float* Z, const float* bias, const float* xhat, const float* rstd,
+                   const float* gamma, int B, int H, float p, uint64_t seed, const uint64_t* dropout_step, int layer,
+                   float* dZ, float* dyx, float* dye, void* stream);
+
+/* actor head: mu = tanh(Z + bias) [B, A <= 64], Normal(mu, exp(clamp(log_std))) log-prob of
+ * act, PPO clipped surrogate vs old_lp / adv; dZ = d loss / d Z, dls = per-row log_std
+ * gradient (entropy bonus included), stats[r] = -min(surr1, surr2) - ent_coef * entropy
+ * (its mean is the actor loss), ent_rows[r] = dist.entropy().mean() */
+int prl_actor_head(const float* Z, const float* bias, const float* log_std, const float* act, const float* old_lp,
+                   const float* adv, int B, int A, float clip, float ent_coef, float* dZ, float* dls, float* stats,
+                   float* ent_rows, void* stream);
+
+/* critic head: v = Z + bias [B], dZ = 2 (v - ret) / B, v and (v - ret)^2 out */
+int prl_critic_head(const float* Z, const float* bias, const float* ret, int B, float* dZ, float* v, float* sq,
+                    void* stream);
+
+/* dst[i][c] = scale[i] * sum_r src[i][r * cols[i] + c] for n <= PRL_MAX_COLSUMS arrays of B rows
+ * (pointer / size arrays are HOST arrays of device pointers; scale may be NULL = 1) */
+int prl_colsums(int n, const float* const* src, const int* cols, const float* scale, float* const* dst, int B,
+                void* stream);
 
 #ifdef __cplusplus
 }

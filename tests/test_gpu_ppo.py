@@ -184,3 +184,35 @@ def test_rollout_trainer_on_env(ppo, reference_semantics, tmp_path):
     assert torch.isfinite(log).all()
     assert torch.isfinite(tr.ep_return).all()
     env.close()
+
+
+@pytest.mark.parametrize("train_critic", [False, True])
+def test_fused_step_matches_autograd(ppo, tmp_path, train_critic):
+    """FusedStep (manual backward, libpianorl kernels between the GEMMs) against the torch
+    autograd step on the same weights and minibatch: logged losses and every gradient. With
+    the critic in train mode dropout is active on both sides with different masks, so there
+    only the actor side (no dropout) is compared."""
+    z = golden()
+    s, a, r, lp, ns, d = golden_batch(z, 0)
+    agents = []
+    for fused in (True, False):
+        ag = _agent(ppo, z, tmp_path, graphs=False)
+        ag.fused = fused
+        if train_critic:
+            ag.critic.train()
+        ag._prepare(s, a, r, lp, ns, d)
+        agents.append(ag)
+    idx = torch.randperm(96, generator=torch.Generator().manual_seed(3))[:32].cuda()
+    rows = []
+    for ag in agents:
+        ag._forward_backward(idx, ag._log_row)
+        torch.cuda.synchronize()
+        rows.append(ag._log_row.cpu().numpy().copy())
+    cols = [0, 2, 4, 5] if train_critic else list(range(6))
+    np.testing.assert_allclose(rows[0][cols], rows[1][cols], rtol=2e-5, atol=2e-6)
+    nets = ("actor",) if train_critic else ("actor", "critic")
+    for net in nets:
+        for (k, p0), (_, p1) in zip(getattr(agents[0], net).named_parameters(), getattr(agents[1], net).named_parameters()):
+            g0, g1 = p0.grad.cpu().numpy(), p1.grad.cpu().numpy()
+            scale = max(np.abs(g1).max(), 1e-6)
+            np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * scale, err_msg=f"{net}.{k}")

@@ -45,6 +45,7 @@ def main():
     p.add_argument("--eager", action="store_true")
     p.add_argument("--blas", default="default", choices=["default", "rocblas", "hipblaslt"])
     p.add_argument("--no-tune", action="store_true", help="no TunableOp GEMM selection")
+    p.add_argument("--autograd", action="store_true", help="torch autograd minibatch step instead of FusedStep")
     args = p.parse_args()
 
     import torch
@@ -70,7 +71,8 @@ def main():
     torch.manual_seed(0)
     agent = ppo.PPOAgent(env.obs_dim, 45, lr=1e-4, gamma=0.99, epsilon=0.2, batch_size=args.batch,
                          ppo_epochs=args.epochs, checkpoint_dir="/tmp/ppo_bench_ckpt", use_wandb=False,
-                         graphs=not args.eager, sample_seed=1000 + rank, tune_gemms=not args.no_tune)
+                         graphs=not args.eager, sample_seed=1000 + rank, tune_gemms=not args.no_tune,
+                         fused=not args.autograd)
     tr = ppo.RolloutTrainer(env, agent, horizon=args.horizon, reference_semantics=args.mode == "reference")
     for _ in range(args.warmup):
         tr.iterate()
@@ -119,7 +121,7 @@ def main():
                        "mode": args.mode, "envs_per_gpu": args.envs, "batch": args.batch, "epochs": args.epochs,
                        "horizon": args.horizon if args.mode == "rollout" else 1,
                        "minibatch_steps_per_update": nmb * args.epochs, "graphs": not args.eager,
-                       "blas": args.blas, "tunableop": not args.no_tune,
+                       "blas": args.blas, "tunableop": not args.no_tune, "fused_step": not args.autograd,
                        "parallelism": f"dp{world}"},
             "phases_ms": {"env_step": t_env * 1e3, "select_actions": t_sel * 1e3,
                           "update_host_wall": upd / args.iters * 1e3},
