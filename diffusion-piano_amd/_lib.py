@@ -91,7 +91,8 @@ def load_rl() -> C.CDLL:
     L.prl_lnrelu_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, u64, vp, i32, vp, vp, vp, vp]
     L.prl_actor_head.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, vp, vp, vp, vp, vp]
     L.prl_critic_head.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
-    L.prl_colsums.argtypes = [i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(f32), C.POINTER(vp), i32, vp]
+    L.prl_colsums.argtypes = [i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(f32), C.POINTER(vp), i32, vp, C.c_size_t,
+                              vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
     _rl = L

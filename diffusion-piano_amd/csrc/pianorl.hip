@@ -458,9 +458,14 @@ struct ColSums {
   const float* src[PRL_MAX_COLSUMS];
   float* dst[PRL_MAX_COLSUMS];
   int cols[PRL_MAX_COLSUMS];
+  int off[PRL_MAX_COLSUMS];  // column offset of entry i in the partials row
   float scale[PRL_MAX_COLSUMS];
-  int n, B;
+  int n, B, chunk, total;
+  float* part;  // [nchunks][total] partial sums (nullptr: one pass, straight to dst)
 };
+constexpr int COLSUM_CHUNK = 128;  // rows per partial sum
+// grid (column blocks, entry, row chunk): a thread sums its column over one chunk of rows in
+// order; with one chunk the result goes straight to dst, else to the partials row
 __global__ void colsums_kernel(ColSums cs) {
   const int i = blockIdx.y;
   if (i >= cs.n) return;
@@ -468,8 +473,20 @@ __global__ void colsums_kernel(ColSums cs) {
   const int C = cs.cols[i];
   if (c >= C) return;
   const float* x = cs.src[i];
+  const int r0 = blockIdx.z * cs.chunk, r1 = min(r0 + cs.chunk, cs.B);
   float acc = 0.f;
-  for (int r = 0; r < cs.B; r++) acc += x[(size_t)r * C + c];
+  for (int r = r0; r < r1; r++) acc += x[(size_t)r * C + c];
+  if (cs.part) cs.part[(size_t)blockIdx.z * cs.total + cs.off[i] + c] = acc;
+  else cs.dst[i][c] = acc * cs.scale[i];
+}
+// the partials of each column summed in chunk order (deterministic)
+__global__ void colsums_final_kernel(ColSums cs, int nchunks) {
+  const int i = blockIdx.y;
+  if (i >= cs.n) return;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cs.cols[i]) return;
+  float acc = 0.f;
+  for (int k = 0; k < nchunks; k++) acc += cs.part[(size_t)k * cs.total + cs.off[i] + c];
   cs.dst[i][c] = acc * cs.scale[i];
 }
 
@@ -598,22 +615,35 @@ int prl_critic_head(const float* Z, const float* bias, const float* ret, int B, 
 }
 
 int prl_colsums(int n, const float* const* src, const int* cols, const float* scale, float* const* dst, int B,
-                void* stream) {
+                float* scratch, size_t scratch_floats, void* stream) {
   if (n <= 0 || n > PRL_MAX_COLSUMS || !src || !cols || !dst || B <= 0) return fail("prl_colsums: bad arguments");
   ColSums cs{};
-  int cmax = 0;
+  int cmax = 0, total = 0;
   for (int i = 0; i < n; i++) {
     if (!src[i] || !dst[i] || cols[i] <= 0) return fail("prl_colsums: bad entry");
     cs.src[i] = src[i];
     cs.dst[i] = dst[i];
     cs.cols[i] = cols[i];
+    cs.off[i] = total;
     cs.scale[i] = scale ? scale[i] : 1.f;
     cmax = cols[i] > cmax ? cols[i] : cmax;
+    total += cols[i];
   }
   cs.n = n;
   cs.B = B;
-  colsums_kernel<<<dim3((cmax + 127) / 128, n), 128, 0, (hipStream_t)stream>>>(cs);
+  cs.total = total;
+  const int nchunks = (B + COLSUM_CHUNK - 1) / COLSUM_CHUNK;
+  cs.chunk = nchunks > 1 ? COLSUM_CHUNK : B;
+  if (nchunks > 1) {
+    if (!scratch || scratch_floats < (size_t)nchunks * total) return fail("prl_colsums: scratch too small");
+    cs.part = scratch;
+  }
+  colsums_kernel<<<dim3((cmax + 127) / 128, n, nchunks > 1 ? nchunks : 1), 128, 0, (hipStream_t)stream>>>(cs);
   HIPCHK(hipGetLastError());
+  if (nchunks > 1) {
+    colsums_final_kernel<<<dim3((cmax + 127) / 128, n), 128, 0, (hipStream_t)stream>>>(cs, nchunks);
+    HIPCHK(hipGetLastError());
+  }
   return 0;
 }
 

@@ -359,6 +359,7 @@ class FusedStep:
         n = len(entries)
         b["_cs"] = ((C.c_void_p * n)(*[e[0].data_ptr() for e in entries]), (C.c_int * n)(*[e[1] for e in entries]),
                     (C.c_float * n)(*[e[2] for e in entries]), (C.c_void_p * n)(*[e[3].data_ptr() for e in entries]), n)
+        b["_scratch"] = torch.empty(((B + 127) // 128) * sum(e[1] for e in entries), **f32)
         self.bufs[B] = b
         return b
 
@@ -413,7 +414,7 @@ class FusedStep:
                 if i > 0:
                     dy = torch.mm(dz, lin.weight, out=b[f"{net}dY{i - 1}"])
         src, cols, scale, dst, n = b["_cs"]
-        chk(R.prl_colsums(n, src, cols, scale, dst, B, st))
+        chk(R.prl_colsums(n, src, cols, scale, dst, B, b["_scratch"].data_ptr(), b["_scratch"].numel(), st))
 
 
 # ---------------------------------------------------------------- the agent (ppo_v2.py:133-336)

@@ -107,9 +107,11 @@ int prl_critic_head(const float* Z, const float* bias, const float* ret, int B, 
                     void* stream);
 
 /* dst[i][c] = scale[i] * sum_r src[i][r * cols[i] + c] for n <= PRL_MAX_COLSUMS arrays of B rows
- * (pointer / size arrays are HOST arrays of device pointers; scale may be NULL = 1) */
+ * (pointer / size arrays are HOST arrays of device pointers; scale may be NULL = 1). Above 128
+ * rows the sum runs in 128-row chunks through scratch (device, >= ceil(B/128) * sum(cols)
+ * floats), summed in chunk order: deterministic for every B. */
 int prl_colsums(int n, const float* const* src, const int* cols, const float* scale, float* const* dst, int B,
-                void* stream);
+                float* scratch, size_t scratch_floats, void* stream);
 
 #ifdef __cplusplus
 }

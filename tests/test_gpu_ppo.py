@@ -216,3 +216,31 @@ def test_fused_step_matches_autograd(ppo, tmp_path, train_critic):
             g0, g1 = p0.grad.cpu().numpy(), p1.grad.cpu().numpy()
             scale = max(np.abs(g1).max(), 1e-6)
             np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * scale, err_msg=f"{net}.{k}")
+
+
+def test_fused_step_large_minibatch(ppo, tmp_path):
+    """B = 512 rows: the column sums run in 128-row chunks (partials + ordered final sum)."""
+    rng = np.random.RandomState(9)
+    n, S = 1024, 64
+    s = rng.rand(n, S).astype(np.float32)
+    a = rng.uniform(-1, 1, (n, 45)).astype(np.float32)
+    lp = rng.uniform(-60, -40, n).astype(np.float32)
+    r, d = rng.rand(n), (rng.rand(n) < 0.1).astype(np.float32)
+    ns = rng.rand(n, S).astype(np.float32)
+    agents = []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        ag = ppo.PPOAgent(S, 45, batch_size=512, ppo_epochs=1, use_wandb=False, checkpoint_dir=str(tmp_path),
+                          graphs=False, fused=fused)
+        ag.critic.eval()
+        ag._prepare(s, a, r, lp, ns, d)
+        agents.append(ag)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(1))[:512].cuda()
+    for ag in agents:
+        ag._forward_backward(idx, ag._log_row)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(agents[0]._log_row.cpu().numpy(), agents[1]._log_row.cpu().numpy(), rtol=2e-5, atol=2e-6)
+    for net in ("actor", "critic"):
+        for (k, p0), (_, p1) in zip(getattr(agents[0], net).named_parameters(), getattr(agents[1], net).named_parameters()):
+            g0, g1 = p0.grad.cpu().numpy(), p1.grad.cpu().numpy()
+            np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * max(np.abs(g1).max(), 1e-6), err_msg=f"{net}.{k}")
