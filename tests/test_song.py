@@ -221,3 +221,19 @@ def test_parse_is_fast(mus):
                                                      DATA / "Guren no Yumiya Cut 14s_fingering v3.txt")
         mus.song_tables(mus.trim_silence(seq), 0.05)
     assert (time.perf_counter() - t0) / 20 < 0.05
+
+
+def test_integration_snippet_runs(mus, monkeypatch):
+    """INTEGRATION.md section 5, executed verbatim (host-only library, no GPU); its tables
+    must equal the package's."""
+    text = (ROOT / "INTEGRATION.md").read_text()
+    block = re.findall(r"```python\n(.*?)```", text, re.S)[4]
+    assert "pss_song_tables" in block
+    monkeypatch.chdir(ROOT)
+    ns = {}
+    exec(block, ns)
+    seq = mus.parse_midi(DATA / "Crossing Field Cut 10s.mid")
+    want = mus.song_tables(mus.trim_silence(seq), 0.05)
+    np.testing.assert_array_equal(ns["goal"], want.goal)
+    np.testing.assert_array_equal(ns["count"], want.count)
+    np.testing.assert_array_equal(ns["keys"], want.keys)
