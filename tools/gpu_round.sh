@@ -8,7 +8,7 @@ P=${1:-r01}
 SONG=crossing_field
 mkdir -p gpurun_out profiles
 rm -rf gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write gpurun_out/${P}_sq
-PIANOSIM_REPORT=profiles/${P}_drift.json timeout -k 10 500 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1
+PIANOSIM_REPORT=profiles/${P}_drift.json timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 RC=$?
 echo "PYTEST_EXIT $RC" >> gpurun_out/pytest_gpu.log
 # 0 = green, 1 = a failed assertion; anything else (fault, abort, time limit) ends the call
@@ -28,5 +28,6 @@ if [ -f diffusion-piano_amd/libpianosim_timing.so ]; then
 fi
 timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 > profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/throughput.py twinkle 1024 4096 >> profiles/${P}_throughput.txt 2>/dev/null || exit 6
+timeout -k 10 200 python tools/ppo_bench.py --mode reference --iters 3 --warmup 2 > profiles/${P}_ppo_bench.jsonl 2>/dev/null || exit 8
 cp -r profiles gpurun_out/profiles_new
 echo DONE
