@@ -62,23 +62,52 @@ def load_song(dp, name):
     return seq, dp.TaskConfig(trim_silence=True)
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads():
+    """The host cores this process may use (the box's CPU share: OMP_NUM_THREADS there)."""
+    n = len(os.sched_getaffinity(0))
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
 def cpu_baseline(dp, seq, task, n_envs, steps):
-    """The fp64 oracle (oracle/pianosim_ref.c), one thread, same song/task, random actions."""
+    """The fp64 oracle (oracle/pianosim_ref.c), one thread (the reference's serial VecEnv),
+    same song/task, random actions; plus the all-cores variant (OpenMP over envs)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import ref  # CPU checker/baseline only
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
-    env = ref.OracleEnv(md, st, tc, n_envs)
-    env.reset()
     lo, hi = dp.model.action_spec(md)
-    rng = np.random.RandomState(12345)
-    acts = [rng.uniform(lo, hi, (n_envs, 45)).astype(np.float32) for _ in range(steps)]
-    t0 = time.perf_counter()
-    for a in acts:
-        env.step(a)
-    dt = time.perf_counter() - t0
-    return {"value": n_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_envs} envs x {steps} random-action control steps, {dt:.1f} s, 1 thread "
-                      f"(fp64 oracle restatement; MuJoCo/dm_control absent)"}
+
+    def run(n, k, threads):
+        env = ref.OracleEnv(md, st, tc, n)
+        env.reset()
+        rng = np.random.RandomState(12345)
+        acts = [rng.uniform(lo, hi, (n, 45)).astype(np.float32) for _ in range(k)]
+        t0 = time.perf_counter()
+        for a in acts:
+            env.step(a, threads=threads)
+        dt = time.perf_counter() - t0
+        return n * k / dt, dt
+
+    v1, dt1 = run(n_envs, steps, 1)
+    out = {"value": v1, "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": f"{n_envs} envs x {steps} random-action control steps, {dt1:.1f} s, 1 thread "
+                     f"(fp64 oracle restatement; MuJoCo/dm_control absent)", "cpu": _cpu_model()}
+    nt = _cpu_threads()
+    if nt > 1:
+        n_all, k_all = 16 * nt, max(50, steps // 5)
+        va, dta = run(n_all, k_all, nt)
+        out["all_cores"] = {"value": va, "unit": "env-steps/s", "cores": nt, "kind": "port",
+                            "sample": f"{n_all} envs x {k_all} steps, {dta:.1f} s, OpenMP over envs"}
+    return out
 
 
 def _profile(name):

@@ -787,8 +787,8 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     }
   }
 
-  ref_rows_hist[ncoup]++;
-  ref_con_hist[E->ncon]++;
+  __atomic_fetch_add(&ref_rows_hist[ncoup], 1, __ATOMIC_RELAXED); /* ref_step_threads runs envs in parallel */
+  __atomic_fetch_add(&ref_con_hist[E->ncon], 1, __ATOMIC_RELAXED);
   /* PGS on the coupled rows; closed-form free key rows */
   double w[NV];
   memset(w, 0, sizeof(w));
@@ -1129,6 +1129,16 @@ void ref_reset(ref_env* R, const uint8_t* mask, float* obs) {
 
 void ref_step(ref_env* R, const float* action, float* obs, float* rew, float* disc, uint8_t* st) {
   int od = ref_obs_dim(R);
+  for (int i = 0; i < R->n; i++)
+    control_step(R, &R->e[i], action + (size_t)i * PS_NACTION, obs + (size_t)i * od, rew + i, disc + i, st + i);
+}
+
+/* The all-cores CPU baseline: the same per-env step, envs spread over
+ * OpenMP threads (envs are independent; per-step scratch is thread-local). */
+void ref_step_threads(ref_env* R, const float* action, float* obs, float* rew, float* disc, uint8_t* st,
+                      int nthreads) {
+  int od = ref_obs_dim(R);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
   for (int i = 0; i < R->n; i++)
     control_step(R, &R->e[i], action + (size_t)i * PS_NACTION, obs + (size_t)i * od, rew + i, disc + i, st + i);
 }

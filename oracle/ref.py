@@ -41,6 +41,7 @@ def lib():
         L.ref_obs_dim.argtypes = [C.c_void_p]
         L.ref_reset.argtypes = [C.c_void_p, C.c_void_p, _f32p]
         L.ref_step.argtypes = [C.c_void_p, _f32p, _f32p, _f32p, _f32p, _u8p]
+        L.ref_step_threads.argtypes = [C.c_void_p, _f32p, _f32p, _f32p, _f32p, _u8p, C.c_int]
         L.ref_get_state.argtypes = [C.c_void_p, _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _u8p]
         L.ref_set_state.argtypes = [C.c_void_p, _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _u8p]
         L.ref_set_applied.argtypes = [C.c_void_p, C.c_void_p]
@@ -92,13 +93,18 @@ class OracleEnv:
         lib().ref_reset(self._h, m, obs)
         return obs
 
-    def step(self, action):
+    def step(self, action, threads: int = 1):
+        """One control step of every env; ``threads > 1`` spreads the envs over OpenMP
+        threads (the all-cores CPU baseline; results identical to the serial loop)."""
         a = np.ascontiguousarray(action, np.float32).reshape(self.n, self.NACTION)
         obs = np.zeros((self.n, self.obs_dim), np.float32)
         rew = np.zeros(self.n, np.float32)
         disc = np.zeros(self.n, np.float32)
         st = np.zeros(self.n, np.uint8)
-        lib().ref_step(self._h, a, obs, rew, disc, st)
+        if threads > 1:
+            lib().ref_step_threads(self._h, a, obs, rew, disc, st, threads)
+        else:
+            lib().ref_step(self._h, a, obs, rew, disc, st)
         return obs, rew, disc, st
 
     def get_state(self):

@@ -184,3 +184,20 @@ def test_oracle_random_rollout_is_stable(dp, ref):
     s = env.get_state()
     assert np.isfinite(s["qpos"]).all() and np.abs(s["qvel"]).max() < 200
     assert np.isfinite(rew).all()
+
+
+def test_threaded_cpu_baseline_matches_serial(dp, ref):
+    """bench.py's all-cores CPU baseline (OpenMP over envs) steps exactly the serial loop."""
+    outs = []
+    for threads in (1, 4):
+        md, st, tc, env = make(dp, ref, "twinkle", n=12)
+        env.reset()
+        lo, hi = dp.model.action_spec(md)
+        rng = np.random.RandomState(3)
+        for _ in range(8):
+            res = env.step(rng.uniform(lo, hi, (12, 45)).astype(np.float32), threads=threads)
+        outs.append((res, env.get_state()))
+    for a, b in zip(outs[0][0], outs[1][0]):
+        np.testing.assert_array_equal(a, b)
+    for k in outs[0][1]:
+        np.testing.assert_array_equal(outs[0][1][k], outs[1][1][k])
