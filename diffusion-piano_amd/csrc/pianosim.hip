@@ -65,6 +65,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
   memset(m, 0, sizeof(*m));
   m->timestep = (float)d->timestep;
   m->nsub = d->n_substeps;
+  if (m->nsub < 1) return fail("n_substeps must be >= 1");
   for (int i = 0; i < 3; i++) m->grav[i] = (float)d->gravity[i];
   for (int k = 0; k < NK; k++) {
     for (int i = 0; i < 3; i++) {
