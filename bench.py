@@ -36,6 +36,7 @@ def bytes_per_env_step(obs_dim):
     return 45 * 4 + 3 * 140 * 4 * 2 + 16 + obs_dim * 4 + 12
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector), spec
 
 
 def parse():
@@ -135,6 +136,20 @@ def issue_summary(n_envs, song):
     return None
 
 
+def valu_roofline(song, n_envs, kernel_ms):
+    """The compute-side roofline: algorithmic FLOPs per env-step from the
+    oracle's counting build (tools/count_flops.py -> profiles/flops.json) over the FP32 vector
+    peak. Like the HBM one it is far from 1: the bound is dependent-op latency per wave."""
+    d = _profile("flops.json")
+    c = d and d.get("configs", {}).get(song)
+    if not c:
+        return None
+    achieved = c["flops_per_env_step"] * n_envs / (kernel_ms * 1e-3) / 1e12
+    return {"bound": "valu", "achieved": achieved, "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP32_VECTOR_PEAK_TFLOPS, "flops_per_env_step": c["flops_per_env_step"],
+            "source": "profiles/flops.json (tools/count_flops.py)"}
+
+
 def drift_summary():
     """qpos L-inf drift vs the fp64 CPU step, from the committed drift report written by
     tests/test_gpu_drift.py (PIANOSIM_REPORT=profiles/drift_latest.json)."""
@@ -228,6 +243,7 @@ def main():
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
                          "kernel_ms_note": "HIP events around ps_step: order_kernel (counting sort, ~5 us) + pianosim_kernel",
                          "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song)},
+            "valu_roofline": valu_roofline(args.song, N, kernel_ms),
             "qpos_drift": drift_summary(),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure

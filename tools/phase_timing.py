@@ -28,3 +28,12 @@ for i, n in names.items():
     v = out[:, i].astype(np.float64)
     print(f"{n:14s} {v.mean()/10:12.0f} cycles/env-step  {100*v.sum()/tot.sum():5.1f}%")
 print(f"total {tot.mean()/10:.0f} cycles/env-step per wave; mean rows/substep {out[:,9].mean()/100:.1f} mean contacts {out[:,10].mean()/100:.2f}")
+# the per-env spread sets the tail of a launch (4096 envs = 2 rounds of 2048 slots)
+per = tot / 10
+q = np.percentile(per, [50, 90, 99, 100])
+top = per >= q[2]
+print(f"per-env cycles/env-step p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f}; "
+      f"rows/substep: all {out[:,9].mean()/100:.1f}, top 1% {out[top,9].mean()/100:.1f}")
+for i, n in names.items():
+    v = out[top, i].astype(np.float64)
+    print(f"  top1% {n:14s} {v.mean()/10:12.0f}")
