@@ -4,7 +4,7 @@ Import with ``importlib.import_module("diffusion-piano_amd")`` (the directory na
 package name required by the build layout).
 """
 
-from . import abi, music, model, evaluation  # noqa: F401
+from . import abi, music, model, mjcf, evaluation  # noqa: F401
 from .envs import (  # noqa: F401
     Array, BatchedPianoEnv, BoundedArray, DEBUG, Environment, StepType, TaskConfig, TimeStep,
     VectorizedPianoEnv, compile_task, load, obs_layout,

@@ -1,0 +1,588 @@
+// pianosim.hip - MI355X (gfx950) batched PianoWithShadowHands step/reset + C-ABI.
+//
+// Device code: prims.h (math, wave primitives, narrow phase) and kernel_v2.inc (the
+// step kernel, one wavefront per env, lane-owned registers, LDS for exchange only).
+// The algorithm and every result-affecting ordering are stated sequentially in the CPU
+// checker; this file adds the host side: descriptor -> device tables,
+// buffers, launches, and the extern "C" entry points of include/pianosim.h.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "devmodel.h"
+#include "prims.h"
+
+using namespace ps;
+
+#include "/tmp/k3.inc"
+
+// ------------------------------------------------------------------ host side
+static thread_local std::string g_err;
+static int fail(const std::string& s) {
+  g_err = s;
+  return -1;
+}
+#define HIPCHK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct ps_env {
+  int n, device, obs_dim;
+  ps_task_cfg cfg;
+  DevModel* d_model;
+  int T;
+  float* d_goal;
+  int *d_count, *d_keys, *d_fingers;
+  float *qpos, *qvel, *qws, *ctrl, *sustain, *applied, *terms, *tips;
+  int *t_idx, *ncon;
+  float *mus_acc, *mus_ep;  // MidiEvaluationWrapper: running sums of this episode, last episode
+  int* mus_cnt;             // finished episodes per env
+  int* order;               // dispatch order of the step launch (longest-expected first)
+  bool ordered;
+  uint8_t* last;
+  bool applied_on;
+};
+
+static void quat2mat_h(const double* q, float* R) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  double w = q[0] / n, x = q[1] / n, y = q[2] / n, z = q[3] / n;
+  double M[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                 2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                 2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+  for (int i = 0; i < 9; i++) R[i] = (float)M[i];
+}
+
+// Derive the flattened device model + topology tables from the descriptor.
+static int build_dev_model(const ps_model_desc* d, DevModel* m) {
+  memset(m, 0, sizeof(*m));
+  m->timestep = (float)d->timestep;
+  m->nsub = d->n_substeps;
+  if (m->nsub < 1) return fail("n_substeps must be >= 1");
+  for (int i = 0; i < 3; i++) m->grav[i] = (float)d->gravity[i];
+  for (int k = 0; k < NK; k++) {
+    for (int i = 0; i < 3; i++) {
+      m->key_pos[k][i] = (float)d->key_pos[k][i];
+      m->key_half[k][i] = (float)d->key_half[k][i];
+      m->key_anchor[k][i] = (float)d->key_anchor[k][i];
+    }
+    double M = d->key_inertia[k] + d->key_armature[k];
+    m->key_mass[k] = (float)d->key_mass[k];
+    m->key_Minv[k] = (float)(1.0 / M);
+    m->key_Mhinv[k] = (float)(1.0 / (M + d->timestep * d->key_damping[k]));
+    m->key_damp[k] = (float)d->key_damping[k];
+    m->key_stiff[k] = (float)d->key_stiffness[k];
+    m->key_sref[k] = (float)d->key_springref[k];
+    m->key_lo[k] = (float)d->key_range[k][0];
+    m->key_hi[k] = (float)d->key_range[k][1];
+    m->key_ylo[k] = (float)(d->key_pos[k][1] - d->key_half[k][1]);
+    m->key_yhi[k] = (float)(d->key_pos[k][1] + d->key_half[k][1]);
+    m->key_binv[k] = (float)d->key_body_invweight[k];
+    m->key_dinv[k] = (float)d->key_dof_invweight[k];
+    if (k > 0 && (m->key_ylo[k] < m->key_ylo[k - 1] || m->key_yhi[k] < m->key_yhi[k - 1]))
+      return fail("keys are not sorted along y");
+  }
+  for (int i = 0; i < 3; i++) { m->base_pos[i] = (float)d->base_pos[i]; m->base_half[i] = (float)d->base_half[i]; }
+  for (int i = 0; i < 2; i++) {
+    m->pc_solref[i] = (float)d->piano_contact.solref[i];
+    m->hc_solref[i] = (float)d->hand_contact.solref[i];
+    m->lim_solref[i] = (float)d->limit_solref[i];
+  }
+  for (int i = 0; i < 5; i++) {
+    m->pc_solimp[i] = (float)d->piano_contact.solimp[i];
+    m->hc_solimp[i] = (float)d->hand_contact.solimp[i];
+    m->lim_solimp[i] = (float)d->limit_solimp[i];
+  }
+  m->pc_fric = (float)d->piano_contact.friction;
+  m->hc_fric = (float)d->hand_contact.friction;
+  // bodies
+  int depth_b[NBT];
+  for (int h = 0; h < NH; h++)
+    for (int b = 0; b < NB; b++) {
+      int B = h * NB + b, p = d->body_parent[h][b];
+      if (p >= b) return fail("bodies must be in tree order");
+      m->body_parent[B] = p < 0 ? -1 : h * NB + p;
+      depth_b[B] = p < 0 ? 0 : depth_b[h * NB + p] + 1;
+      for (int i = 0; i < 3; i++) {
+        m->body_pos[B][i] = (float)d->body_pos[h][b][i];
+        m->body_ipos[B][i] = (float)d->body_ipos[h][b][i];
+      }
+      quat2mat_h(d->body_quat[h][b], m->body_Q[B]);
+      m->body_mass[B] = (float)d->body_mass[h][b];
+      for (int i = 0; i < 6; i++) m->body_I[B][i] = (float)d->body_inertia[h][b][i];
+      m->body_binv[B] = (float)d->body_invweight[h][b];
+      m->body_dof[B] = -1;
+    }
+  int maxlev = 0;
+  for (int B = 0; B < NBT; B++) maxlev = depth_b[B] > maxlev ? depth_b[B] : maxlev;
+  if (maxlev + 1 > MAXLEV) return fail("body tree too deep");
+  m->nlev = maxlev + 1;
+  int n = 0;
+  for (int L = 0; L <= maxlev; L++) {
+    m->lev_start[L] = n;
+    for (int B = 0; B < NBT; B++)
+      if (depth_b[B] == L) m->lev_body[n++] = B;
+    if (n - m->lev_start[L] > 64) return fail("too many bodies in one level");
+  }
+  m->lev_start[maxlev + 1] = n;
+  for (int B = 0; B < NBT; B++) {
+    int p = m->body_parent[B];
+    if (p >= 0) {
+      if (m->body_nchild[p] >= MAXCHILD) return fail("too many children");
+      m->body_child[p][m->body_nchild[p]++] = B;
+    }
+  }
+  // dofs
+  for (int h = 0; h < NH; h++)
+    for (int j = 0; j < ND; j++) {
+      int g = h * ND + j, B = h * NB + d->dof_body[h][j];
+      m->dof_body[g] = B;
+      m->dof_type[g] = d->dof_type[h][j];
+      m->dof_limited[g] = d->dof_limited[h][j];
+      for (int i = 0; i < 3; i++) m->dof_axis[g][i] = (float)d->dof_axis[h][j][i];
+      m->dof_lo[g] = (float)d->dof_range[h][j][0];
+      m->dof_hi[g] = (float)d->dof_range[h][j][1];
+      m->dof_damp[g] = (float)d->dof_damping[h][j];
+      m->dof_arm[g] = (float)d->dof_armature[h][j];
+      m->dof_dinv[g] = (float)d->dof_invweight[h][j];
+      if (m->body_dof[B] < 0) m->body_dof[B] = g;
+      else if (m->body_dof[B] + m->body_ndof[B] != g) return fail("dofs of a body must be contiguous");
+      m->body_ndof[B]++;
+      m->obs_dof[g] = h * ND + d->dof_obs_order[h][j];
+      m->dof_act[g] = -1;
+    }
+  for (int B = 0; B < NBT; B++) {
+    if (m->body_parent[B] >= 0 && m->body_ndof[B] != 1) return fail("non-root bodies need exactly one hinge");
+    if (m->body_parent[B] >= 0 && m->dof_type[m->body_dof[B]] != 0) return fail("non-root dofs must be hinges");
+    if (m->body_parent[B] < 0)
+      for (int j = 0; j < m->body_ndof[B]; j++)
+        if (m->dof_type[m->body_dof[B] + j] != 1) return fail("root dofs must be slides");
+  }
+  // dof parent / ancestors / depth / descendants
+  int dpar[NDT];
+  for (int g = 0; g < NDT; g++) {
+    int B = m->dof_body[g];
+    if (g > m->body_dof[B]) { dpar[g] = g - 1; continue; }
+    int p = m->body_parent[B], par = -1;
+    while (p >= 0) {
+      if (m->body_ndof[p] > 0) { par = m->body_dof[p] + m->body_ndof[p] - 1; break; }
+      p = m->body_parent[p];
+    }
+    dpar[g] = par;
+  }
+  int maxdep = 0;
+  for (int g = 0; g < NDT; g++) {
+    int a = 0;
+    for (int x = g; x >= 0; x = dpar[x]) {
+      if (a >= MAXDEP) return fail("dof tree too deep");
+      m->dof_anc[g][a++] = x;
+      m->dof_ancmask[g] |= 1ull << x;
+    }
+    for (int r = a; r < MAXDEP; r++) m->dof_anc[g][r] = -1;
+    m->dof_depth[g] = a - 1;
+    maxdep = a - 1 > maxdep ? a - 1 : maxdep;
+  }
+  for (int g = 0; g < NDT; g++)
+    for (int a = 1; a <= m->dof_depth[g]; a++) {
+      int i = m->dof_anc[g][a];
+      m->dof_desc[i][m->dof_ndesc[i]++] = g;
+      m->dof_descmask[i] |= 1ull << g;
+    }
+  m->ndepth = maxdep + 1;
+  n = 0;
+  for (int dd = 0; dd <= maxdep; dd++) {
+    m->dep_start[dd] = n;
+    for (int g = 0; g < NDT; g++)
+      if (m->dof_depth[g] == dd) m->dep_dof[n++] = g;
+  }
+  m->dep_start[maxdep + 1] = n;
+  for (int B = 0; B < NBT; B++) {
+    uint64_t mask = 0;
+    for (int x = B; x >= 0; x = m->body_parent[x])
+      for (int j = 0; j < m->body_ndof[x]; j++) mask |= 1ull << (m->body_dof[x] + j);
+    m->body_pathmask[B] = mask;
+  }
+  int t = 0;
+  for (int a = 1; a < MAXDEP; a++)
+    for (int b = a; b < MAXDEP; b++) { m->tri_a[t] = a; m->tri_b[t] = b; t++; }
+  // ordering must be: all pairs with b <= dk come first for any dk -> sort by b
+  {
+    int ta[NTRI], tb[NTRI], c = 0;
+    for (int b = 1; b < MAXDEP; b++)
+      for (int a = 1; a <= b; a++) { ta[c] = a; tb[c] = b; c++; }
+    for (int i = 0; i < NTRI; i++) { m->tri_a[i] = ta[i]; m->tri_b[i] = tb[i]; }
+  }
+  // actuators + tendons
+  for (int h = 0; h < NH; h++)
+    for (int a = 0; a < NA; a++) {
+      int A = h * NA + a, tg = d->act_target[h][a];
+      m->act_kind[A] = d->act_kind[h][a];
+      if (d->act_kind[h][a] == 0) {
+        m->act_dof0[A] = h * ND + tg;
+        m->act_c0[A] = 1.f;
+        m->act_dof1[A] = h * ND + tg;
+        m->act_c1[A] = 0.f;
+      } else {
+        m->act_dof0[A] = h * ND + d->tendon_dof[h][tg][0];
+        m->act_c0[A] = (float)d->tendon_coef[h][tg][0];
+        m->act_dof1[A] = h * ND + d->tendon_dof[h][tg][1];
+        m->act_c1[A] = (float)d->tendon_coef[h][tg][1];
+      }
+      m->act_kp[A] = (float)d->act_kp[h][a];
+      m->act_clo[A] = (float)d->act_ctrlrange[h][a][0];
+      m->act_chi[A] = (float)d->act_ctrlrange[h][a][1];
+      m->act_flim[A] = d->act_forcelimited[h][a];
+      m->act_flo[A] = (float)d->act_forcerange[h][a][0];
+      m->act_fhi[A] = (float)d->act_forcerange[h][a][1];
+      int dofs[2] = {m->act_dof0[A], m->act_dof1[A]};
+      float cs[2] = {m->act_c0[A], m->act_c1[A]};
+      for (int i = 0; i < (m->act_kind[A] == 1 ? 2 : 1); i++) {
+        if (m->dof_act[dofs[i]] >= 0) return fail("a dof may be driven by at most one actuator");
+        m->dof_act[dofs[i]] = A;
+        m->dof_act_coef[dofs[i]] = cs[i];
+      }
+    }
+  // geoms, sites, pairs
+  for (int h = 0; h < NH; h++)
+    for (int g = 0; g < NG; g++) {
+      int G = h * NG + g;
+      m->geom_body[G] = h * NB + d->geom_body[h][g];
+      for (int i = 0; i < 3; i++) {
+        m->geom_pos[G][i] = (float)d->geom_pos[h][g][i];
+        m->geom_axis[G][i] = (float)d->geom_axis[h][g][i];
+      }
+      m->geom_hl[G] = (float)d->geom_halflen[h][g];
+      m->geom_r[G] = (float)d->geom_radius[h][g];
+    }
+  m->root_geom_count = d->root_geom_count;
+  // v2 packed lane topology + conservative piano prefilter bounds
+  for (int B = 0; B < NBT; B++) {
+    m->body_level[B] = depth_b[B];
+    int pk = 0;
+    for (int c = 0; c < m->body_nchild[B]; c++) pk |= m->body_child[B][c] << (6 * c);
+    m->body_child_pack[B] = pk;
+  }
+  for (int g = 0; g < NDT; g++) {
+    int p[2] = {0, 0};
+    for (int a = 1; a < MAXDEP; a++) {
+      int v = a <= m->dof_depth[g] ? m->dof_anc[g][a] : 255;
+      p[(a - 1) / 4] |= v << (8 * ((a - 1) % 4));
+    }
+    m->dof_anc_pack[g][0] = p[0];
+    m->dof_anc_pack[g][1] = p[1];
+    m->dof_anc_pack[g][2] = 0;
+  }
+  {
+    float zmax = m->base_pos[2] + m->base_half[2], xmin = m->base_pos[0] - m->base_half[0],
+          xmax = m->base_pos[0] + m->base_half[0];
+    for (int k = 0; k < NK; k++) {
+      zmax = fmaxf(zmax, m->key_pos[k][2] + m->key_half[k][2] + 0.02f);
+      xmin = fminf(xmin, m->key_pos[k][0] - m->key_half[k][0] - 0.02f);
+      xmax = fmaxf(xmax, m->key_pos[k][0] + m->key_half[k][0] + 0.02f);
+    }
+    m->key_top_zmax = zmax;
+    m->piano_xmin = xmin;
+    m->piano_xmax = xmax;
+  }
+  for (int k = 0; k < NK; k++) {
+    float* g = m->key_geo[k];
+    for (int i = 0; i < 3; i++) { g[i] = m->key_pos[k][i]; g[3 + i] = m->key_half[k][i]; g[6 + i] = m->key_anchor[k][i]; }
+    g[9] = m->key_pos[k][0] - m->key_half[k][0] - 0.02f;
+    g[10] = m->key_pos[k][0] + m->key_half[k][0] + 0.02f;
+    g[11] = m->key_ylo[k];
+    g[12] = m->key_yhi[k];
+    g[13] = m->key_pos[k][2] + m->key_half[k][2] + 0.02f;
+    g[14] = g[15] = 0.f;
+  }
+  {
+    double y0 = m->key_ylo[0], y1 = m->key_yhi[NK - 1];
+    for (int k = 0; k < NK; k++) { y0 = fmin(y0, m->key_ylo[k]); y1 = fmax(y1, m->key_yhi[k]); }
+    double bw = (y1 - y0) / NKB;
+    m->kb_y0 = (float)y0;
+    m->kb_inv = (float)(1.0 / bw);
+    for (int b = 0; b < NKB; b++) {
+      double blo = y0 + b * bw, bhi = blo + bw;
+      int f = 0;
+      while (f < NK && m->key_yhi[f] < blo) f++;
+      int e = f;
+      while (e < NK && m->key_ylo[e] <= bhi) e++;
+      m->kb_first[b] = (uint8_t)f;
+      m->kb_end[b] = (uint8_t)e;
+    }
+  }
+  for (int h = 0; h < NH; h++)
+    for (int s = 0; s < PS_NFINGER; s++) {
+      m->site_body[h * PS_NFINGER + s] = h * NB + d->site_body[h][s];
+      for (int i = 0; i < 3; i++) m->site_pos[h * PS_NFINGER + s][i] = (float)d->site_pos[h][s][i];
+    }
+  if (d->n_cappairs < 0 || d->n_cappairs > PS_MAX_CAPPAIRS) return fail("bad n_cappairs");
+  m->npairs = d->n_cappairs;
+  for (int i = 0; i < d->n_cappairs; i++) {
+    m->pair[i][0] = d->cappair[i][0];
+    m->pair[i][1] = d->cappair[i][1];
+    if (m->pair[i][0] < 0 || m->pair[i][0] >= NGT || m->pair[i][1] < 0 || m->pair[i][1] >= NGT)
+      return fail("capsule pair index out of range");
+  }
+  // the cross-hand pairs can be skipped wholesale when the hands' boxes are apart, if they
+  // all come after the same-hand ones (model.capsule_pairs orders them so)
+  m->npairs_same = 0;
+  while (m->npairs_same < m->npairs && m->pair[m->npairs_same][0] / NG == m->pair[m->npairs_same][1] / NG)
+    m->npairs_same++;
+  for (int i = m->npairs_same; i < m->npairs; i++)
+    if (m->pair[i][0] / NG == m->pair[i][1] / NG) { m->npairs_same = m->npairs; break; }
+  return 0;
+}
+
+extern "C" {
+
+const char* ps_last_error(void) { return g_err.c_str(); }
+int ps_version(void) { return 1; }
+int ps_model_desc_size(void) { return (int)sizeof(ps_model_desc); }
+int ps_obs_dim(const ps_task_cfg* cfg) {
+  return (cfg->n_steps_lookahead + 1) * (NK + 1) + (cfg->fingering_reward ? 10 : 0) + NK + 1 + NH * ND;
+}
+
+int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_task_cfg* cfg, int n_envs, int device,
+              uint64_t seed, ps_env** out) {
+  (void)seed;
+  if (!model || !song || !cfg || !out) return fail("null argument");
+  if (n_envs <= 0) return fail("n_envs must be positive");
+  if (song->T <= 0) return fail("empty song");
+  if (cfg->n_steps_lookahead < 0) return fail("negative lookahead");
+  if (cfg->max_contacts < 0 || cfg->max_contacts > MAXCON) return fail("max_contacts out of range");
+  if (cfg->pgs_iterations < 0) return fail("negative pgs_iterations");
+  for (int t = 0; t < song->T; t++)
+    if (song->count[t] < 0 || song->count[t] > PS_MAX_NOTES) return fail("bad note count");
+  HIPCHK(hipSetDevice(device));
+  DevModel* hm = new DevModel;
+  if (build_dev_model(model, hm)) { delete hm; return -1; }
+  ps_env* E = new ps_env();
+  E->n = n_envs;
+  E->device = device;
+  E->cfg = *cfg;
+  E->obs_dim = ps_obs_dim(cfg);
+  E->T = song->T;
+  size_t N = (size_t)n_envs;
+  HIPCHK(hipMalloc(&E->d_model, sizeof(DevModel)));
+  HIPCHK(hipMemcpy(E->d_model, hm, sizeof(DevModel), hipMemcpyHostToDevice));
+  delete hm;
+  HIPCHK(hipMalloc(&E->d_goal, sizeof(float) * song->T * (NK + 1)));
+  HIPCHK(hipMemcpy(E->d_goal, song->goal, sizeof(float) * song->T * (NK + 1), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&E->d_count, sizeof(int) * song->T));
+  HIPCHK(hipMemcpy(E->d_count, song->count, sizeof(int) * song->T, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&E->d_keys, sizeof(int) * song->T * PS_MAX_NOTES));
+  HIPCHK(hipMemcpy(E->d_keys, song->keys, sizeof(int) * song->T * PS_MAX_NOTES, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&E->d_fingers, sizeof(int) * song->T * PS_MAX_NOTES));
+  HIPCHK(hipMemcpy(E->d_fingers, song->fingers, sizeof(int) * song->T * PS_MAX_NOTES, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&E->qpos, sizeof(float) * N * NV));
+  HIPCHK(hipMalloc(&E->qvel, sizeof(float) * N * NV));
+  HIPCHK(hipMalloc(&E->qws, sizeof(float) * N * NV));
+  HIPCHK(hipMalloc(&E->applied, sizeof(float) * N * NV));
+  HIPCHK(hipMalloc(&E->ctrl, sizeof(float) * N * NU));
+  HIPCHK(hipMalloc(&E->sustain, sizeof(float) * N));
+  HIPCHK(hipMalloc(&E->terms, sizeof(float) * N * PS_NTERMS));
+  HIPCHK(hipMalloc(&E->tips, sizeof(float) * N * 2 * PS_NFINGER * 3));
+  HIPCHK(hipMalloc(&E->t_idx, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->ncon, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->mus_acc, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMalloc(&E->mus_ep, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMalloc(&E->mus_cnt, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->order, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->last, N));
+  HIPCHK(hipMemset(E->qpos, 0, sizeof(float) * N * NV));
+  HIPCHK(hipMemset(E->qvel, 0, sizeof(float) * N * NV));
+  HIPCHK(hipMemset(E->qws, 0, sizeof(float) * N * NV));
+  HIPCHK(hipMemset(E->applied, 0, sizeof(float) * N * NV));
+  HIPCHK(hipMemset(E->ctrl, 0, sizeof(float) * N * NU));
+  HIPCHK(hipMemset(E->sustain, 0, sizeof(float) * N));
+  HIPCHK(hipMemset(E->terms, 0, sizeof(float) * N * PS_NTERMS));
+  HIPCHK(hipMemset(E->tips, 0, sizeof(float) * N * 2 * PS_NFINGER * 3));
+  HIPCHK(hipMemset(E->t_idx, 0, sizeof(int) * N));
+  HIPCHK(hipMemset(E->ncon, 0, sizeof(int) * N));
+  HIPCHK(hipMemset(E->mus_acc, 0, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMemset(E->mus_ep, 0, sizeof(float) * N * PS_NMUSIC));
+  HIPCHK(hipMemset(E->mus_cnt, 0, sizeof(int) * N));
+  HIPCHK(hipMemset(E->last, 0, N));
+  HIPCHK(hipDeviceSynchronize());
+  E->applied_on = false;
+  E->ordered = !(getenv("PIANOSIM_NO_ORDER") && atoi(getenv("PIANOSIM_NO_ORDER")));
+  *out = E;
+  return 0;
+}
+
+void ps_destroy(ps_env* E) {
+  if (!E) return;
+  (void)hipSetDevice(E->device);
+  hipFree(E->d_model); hipFree(E->d_goal); hipFree(E->d_count); hipFree(E->d_keys); hipFree(E->d_fingers);
+  hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
+  hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
+  hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
+  delete E;
+}
+
+// Dispatch order of a step launch: envs by their last contact count, descending, envs about
+// to auto-reset (no physics this step) last. Workgroups are dispatched in blockIdx order, so
+// the expensive envs start in the first wave of workgroups and the cheap ones fill the slots
+// freed late (longest-processing-time-first): the launch's tail is shorter. Each env's
+// result is independent of the order.
+constexpr int ORDER_THREADS = 1024;
+__global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restrict__ ncon,
+                                                              const uint8_t* __restrict__ last,
+                                                              int* __restrict__ order, int n) {
+  constexpr int NB = MAXCON + 2;  // bucket 0: resets, 1 + c: c contacts
+  __shared__ int hist[NB], base[NB];
+  if (threadIdx.x < NB) hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int b = last[e] ? 0 : 1 + min(max(ncon[e], 0), MAXCON);
+    atomicAdd(&hist[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = NB - 1; b >= 0; b--) {  // most contacts first, resets last
+      base[b] = acc;
+      acc += hist[b];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int b = last[e] ? 0 : 1 + min(max(ncon[e], 0), MAXCON);
+    order[atomicAdd(&base[b], 1)] = e;
+  }
+}
+
+static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask, float* obs, float* reward,
+                  float* discount, uint8_t* step_type, void* stream) {
+  Song song{E->T, E->d_goal, E->d_count, E->d_keys, E->d_fingers};
+  Cfg cfg{E->cfg.n_steps_lookahead, E->cfg.fingering_reward, E->cfg.forearm_reward, E->cfg.wrong_press_termination,
+          E->cfg.pgs_iterations, E->cfg.max_contacts, E->obs_dim, E->cfg.canonical_actions,
+          (float)E->cfg.energy_penalty_coef, 0};
+  if (const char* sk = getenv("PIANOSIM_SKIP")) cfg.skip = atoi(sk);
+  Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
+         E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt};
+  const int* order = nullptr;
+  if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
+    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->ncon, E->last, E->order,
+                       E->n);
+    HIPCHK(hipGetLastError());
+    order = E->order;
+  }
+  hipLaunchKernelGGL(pianosim_kernel, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b, action,
+                     mask, obs, reward, discount, step_type, mode, E->n, order);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ps_reset(ps_env* E, const uint8_t* env_mask, float* obs, void* stream) {
+  if (!E || !obs) return fail("null argument");
+  return launch(E, 1, nullptr, env_mask, obs, nullptr, nullptr, nullptr, stream);
+}
+
+int ps_step(ps_env* E, const float* action, float* obs, float* reward, float* discount, uint8_t* step_type,
+            void* stream) {
+  if (!E || !action || !obs || !reward || !discount || !step_type) return fail("null argument");
+  return launch(E, 0, action, nullptr, obs, reward, discount, step_type, stream);
+}
+
+int ps_get_state(ps_env* E, float* qpos, float* qvel, float* qacc_ws, float* ctrl, float* sustain, int32_t* t_idx,
+                 uint8_t* last, void* stream) {
+  if (!E) return fail("null env");
+  hipStream_t s = (hipStream_t)stream;
+  size_t N = E->n;
+  if (qpos) HIPCHK(hipMemcpyAsync(qpos, E->qpos, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
+  if (qvel) HIPCHK(hipMemcpyAsync(qvel, E->qvel, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
+  if (qacc_ws) HIPCHK(hipMemcpyAsync(qacc_ws, E->qws, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
+  if (ctrl) HIPCHK(hipMemcpyAsync(ctrl, E->ctrl, sizeof(float) * N * NU, hipMemcpyDeviceToDevice, s));
+  if (sustain) HIPCHK(hipMemcpyAsync(sustain, E->sustain, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+  if (t_idx) HIPCHK(hipMemcpyAsync(t_idx, E->t_idx, sizeof(int) * N, hipMemcpyDeviceToDevice, s));
+  if (last) HIPCHK(hipMemcpyAsync(last, E->last, N, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+int ps_set_state(ps_env* E, const float* qpos, const float* qvel, const float* qacc_ws, const float* ctrl,
+                 const float* sustain, const int32_t* t_idx, const uint8_t* last, void* stream) {
+  if (!E) return fail("null env");
+  hipStream_t s = (hipStream_t)stream;
+  size_t N = E->n;
+  if (qpos) HIPCHK(hipMemcpyAsync(E->qpos, qpos, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
+  if (qvel) HIPCHK(hipMemcpyAsync(E->qvel, qvel, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
+  if (qacc_ws) HIPCHK(hipMemcpyAsync(E->qws, qacc_ws, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
+  if (ctrl) HIPCHK(hipMemcpyAsync(E->ctrl, ctrl, sizeof(float) * N * NU, hipMemcpyDeviceToDevice, s));
+  if (sustain) HIPCHK(hipMemcpyAsync(E->sustain, sustain, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+  if (t_idx) HIPCHK(hipMemcpyAsync(E->t_idx, t_idx, sizeof(int) * N, hipMemcpyDeviceToDevice, s));
+  if (last) HIPCHK(hipMemcpyAsync(E->last, last, N, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+int ps_set_applied(ps_env* E, const float* qfrc_applied, void* stream) {
+  if (!E) return fail("null env");
+  if (!qfrc_applied) {
+    E->applied_on = false;
+    return 0;
+  }
+  HIPCHK(hipMemcpyAsync(E->applied, qfrc_applied, sizeof(float) * E->n * NV, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
+  E->applied_on = true;
+  return 0;
+}
+
+int ps_reward_terms(ps_env* E, float* terms, void* stream) {
+  if (!E || !terms) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(terms, E->terms, sizeof(float) * E->n * PS_NTERMS, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
+  return 0;
+}
+
+int ps_fingertips(ps_env* E, float* xpos, void* stream) {
+  if (!E || !xpos) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(xpos, E->tips, sizeof(float) * E->n * 2 * PS_NFINGER * 3, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
+  return 0;
+}
+
+#ifdef PS_TIMING
+// diagnostic: per-env phase cycle sums [n][NPHASE] since the last call (host buffer)
+int ps_debug_timing(ps_env* E, uint64_t* out) {
+  static uint64_t* d = nullptr;
+  static size_t cap = 0;
+  size_t bytes = sizeof(uint64_t) * E->n * NPHASE;
+  if (cap < bytes) {
+    if (d) (void)hipFree(d);
+    HIPCHK(hipMalloc(&d, bytes));
+    cap = bytes;
+    HIPCHK(hipMemset(d, 0, bytes));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_timing), &d, sizeof(d)));
+    return 0;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  if (out) HIPCHK(hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(d, 0, bytes));
+  return 0;
+}
+#endif
+
+int ps_musical_metrics(ps_env* E, float* episode, int32_t* episodes, void* stream) {
+  if (!E) return fail("null argument");
+  if (episode)
+    HIPCHK(hipMemcpyAsync(episode, E->mus_ep, sizeof(float) * E->n * PS_NMUSIC, hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
+  if (episodes)
+    HIPCHK(hipMemcpyAsync(episodes, E->mus_cnt, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+int ps_contact_count(ps_env* E, int32_t* ncon, void* stream) {
+  if (!E || !ncon) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(ncon, E->ncon, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -97,6 +97,7 @@ class TaskConfig:
     physics_timestep: float = model_lib.PHYSICS_TIMESTEP
     pgs_iterations: int = 20
     max_contacts: int = 20
+    hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
 
     def lookahead(self) -> int:
         if self.n_seconds_lookahead is not None:
@@ -121,9 +122,13 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
         if cfg.trim_silence:
             seq = music.trim_silence(seq)
         song = music.song_tables(seq, cfg.control_timestep, cfg.initial_buffer_time)
+    hand = None
+    if cfg.hand_xml is not None:
+        from . import mjcf
+        hand = mjcf.load_hand(cfg.hand_xml)
     md = model_lib.build_model(control_timestep=cfg.control_timestep,
                                physics_timestep=cfg.physics_timestep,
-                               hand_collisions=not cfg.disable_hand_collisions)
+                               hand_collisions=not cfg.disable_hand_collisions, hand=hand)
     tc = abi.TaskCfg()
     tc.n_steps_lookahead = cfg.lookahead()
     tc.fingering_reward = int(not cfg.disable_fingering_reward and song.has_fingering)

@@ -1,0 +1,430 @@
+"""MJCF-subset loader for user-supplied hand models.
+
+The reference builds each hand with ``mjcf.from_path`` on the Menagerie Shadow Hand XML and
+then edits it (robopianist/models/hands/shadow_hand.py:93-311): forearm DOFs with position
+actuators and critical damping (``_add_dofs`` :272-311), fingertip sites on the distal
+bodies (:181-198), and capsule fingertip colliders under ``primitive_fingertip_collisions``
+(:144-152). ``load_hand`` reads such an XML into the ``model.HandSpec`` that
+``model.build_model(hand=...)`` compiles. The right hand is read, and the left hand is its
+mirror image, as for the authored hand. ``hand_to_mjcf`` writes a HandSpec back out as
+Menagerie-style MJCF.
+
+The supported subset is what the hot path simulates:
+
+* ``<compiler angle autolimits eulerseq>``;
+* ``<default>`` classes, nested (inheriting) and selected by ``class`` / ``childclass``;
+* ``<body pos quat|euler|axisangle|zaxis>`` with ``<inertial pos quat mass diaginertia|fullinertia>``;
+* ``<joint type=hinge|slide axis range damping armature>``, and ``stiffness`` must be 0;
+* ``<geom>`` colliders (contype or conaffinity non-zero): capsules (``size`` + frame, or
+  ``fromto``) and cylinders, which become capsules as in the reference's MJX path
+  (parallelized_base.py:49-64). Non-colliding (visual) geoms are skipped. Any other
+  collider type raises ``ValueError``, because the kernel has no mesh/box hand colliders;
+* ``<tendon><fixed>`` over two joints;
+* ``<actuator><position joint|tendon kp ctrlrange forcerange>``;
+* ``<contact><exclude body1 body2>``.
+
+The ABI fixes the hand's sizes (``abi.HAND_NBODY`` bodies, ``HAND_NDOF`` - 2 joints,
+``HAND_NGEOM`` capsules, ``HAND_NACT`` - 2 actuators, ``HAND_NTENDON`` tendons), and a
+model that differs raises ``ValueError`` naming the count.
+"""
+
+from __future__ import annotations
+
+import math
+import xml.etree.ElementTree as ET
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from . import abi
+from . import model as M
+
+# shadow_hand_constants.py:33-40 (order matters: site index = finger index)
+FINGERTIP_BODIES = ("thdistal", "ffdistal", "mfdistal", "rfdistal", "lfdistal")
+# shadow_hand.py:41-53: the two default forearm DOFs (stiffness = position-actuator kp)
+FOREARM_DOFS = (("forearm_tx", 1, (-1.0, 0.0, 0.0), (-1.0, 1.0)),
+                ("forearm_ty", 1, (0.0, 0.0, 1.0), M.FOREARM_TY_RANGE))
+
+
+# ------------------------------------------------------------------ small helpers
+def _floats(s: Optional[str]) -> Optional[List[float]]:
+    return None if s is None else [float(x) for x in s.split()]
+
+
+def _qmul(a, b):
+    w1, x1, y1, z1 = a
+    w2, x2, y2, z2 = b
+    return (w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+            w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2)
+
+
+def _axis_quat(axis, angle):
+    a = np.asarray(axis, np.float64)
+    a = a / np.linalg.norm(a)
+    s = math.sin(angle / 2)
+    return (math.cos(angle / 2), a[0] * s, a[1] * s, a[2] * s)
+
+
+def _quat_from_z(z):
+    """The minimal rotation taking +z to ``z`` (MuJoCo's zaxis / fromto frame)."""
+    z = np.asarray(z, np.float64)
+    z = z / np.linalg.norm(z)
+    c = float(z[2])
+    if c > 1.0 - 1e-15:
+        return (1.0, 0.0, 0.0, 0.0)
+    if c < -1.0 + 1e-15:
+        return (0.0, 1.0, 0.0, 0.0)
+    axis = np.cross([0.0, 0.0, 1.0], z)
+    return _axis_quat(axis, math.acos(c))
+
+
+class _Ctx:
+    def __init__(self, root: ET.Element):
+        comp = root.find("compiler")
+        get = comp.get if comp is not None else (lambda k, d=None: d)
+        self.degree = get("angle", "degree") == "degree"   # MJCF's default unit is degrees
+        self.autolimits = get("autolimits", "true") == "true"
+        self.eulerseq = get("eulerseq", "xyz")
+        self.classes: Dict[str, Dict[str, Dict[str, str]]] = {}
+        d = root.find("default")
+        if d is not None:
+            self._defaults(d, {}, "main")
+
+    def _defaults(self, node, inherited, name):
+        own = {tag: dict(attrs) for tag, attrs in inherited.items()}
+        for child in node:
+            if child.tag != "default":
+                own.setdefault(child.tag, {}).update(child.attrib)
+        self.classes[name] = own
+        for child in node:
+            if child.tag == "default":
+                cname = child.get("class")
+                if not cname:
+                    raise ValueError("nested <default> without a class name")
+                self._defaults(child, own, cname)
+
+    def attrs(self, el: ET.Element, tag: str, cls: str) -> Dict[str, str]:
+        cls = el.get("class", cls)
+        if cls not in self.classes and cls != "main":
+            raise ValueError(f"<{el.tag}> uses unknown default class {cls!r}")
+        out = dict(self.classes.get(cls, {}).get(tag, {}))
+        out.update(el.attrib)
+        return out
+
+    def angle(self, v: float) -> float:
+        return math.radians(v) if self.degree else v
+
+    def frame_quat(self, a: Dict[str, str]):
+        if "quat" in a:
+            return tuple(_floats(a["quat"]))
+        if "axisangle" in a:
+            x, y, z, t = _floats(a["axisangle"])
+            return _axis_quat((x, y, z), self.angle(t))
+        if "euler" in a:
+            q = (1.0, 0.0, 0.0, 0.0)
+            for ax, t in zip(self.eulerseq, _floats(a["euler"])):
+                unit = {"x": (1, 0, 0), "y": (0, 1, 0), "z": (0, 0, 1)}[ax.lower()]
+                r = _axis_quat(unit, self.angle(t))
+                q = _qmul(q, r) if ax.islower() else _qmul(r, q)   # lower case: rotating axes
+            return q
+        if "zaxis" in a:
+            return _quat_from_z(_floats(a["zaxis"]))
+        if "xyaxes" in a:
+            v = _floats(a["xyaxes"])
+            x = np.asarray(v[:3]) / np.linalg.norm(v[:3])
+            y = np.asarray(v[3:]) - x * np.dot(x, v[3:])
+            y /= np.linalg.norm(y)
+            return _mat_quat(np.stack([x, y, np.cross(x, y)], axis=1))
+        return (1.0, 0.0, 0.0, 0.0)
+
+    def limited(self, a: Dict[str, str], flag: str, rng: str) -> bool:
+        v = a.get(flag, "auto")
+        if v == "auto":
+            if not self.autolimits and rng in a:
+                raise ValueError(f"{rng} given without {flag} and autolimits is false")
+            return rng in a
+        return v == "true"
+
+
+def _mat_quat(R):
+    w = math.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
+    if w > 1e-8:
+        return (w, (R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w), (R[1, 0] - R[0, 1]) / (4 * w))
+    i = int(np.argmax(np.diag(R)))
+    j, k = (i + 1) % 3, (i + 2) % 3
+    s = math.sqrt(max(0.0, 1.0 + R[i, i] - R[j, j] - R[k, k])) * 2
+    q = [0.0, 0.0, 0.0, 0.0]
+    q[0] = (R[k, j] - R[j, k]) / s
+    q[1 + i] = s / 4
+    q[1 + j] = (R[j, i] + R[i, j]) / s
+    q[1 + k] = (R[k, i] + R[i, k]) / s
+    return tuple(q)
+
+
+def _strip(name: Optional[str], prefix: str) -> Optional[str]:
+    if name is not None and prefix and name.startswith(prefix):
+        return name[len(prefix):]
+    return name
+
+
+# ------------------------------------------------------------------ loader
+def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
+    """Read a right-hand MJCF (a path, or the XML text itself) into a ``model.HandSpec``,
+    with the reference's forearm DOFs and fingertip sites added (shadow_hand.py:181-198,
+    272-311). ``prefix`` is stripped from element names (Menagerie's ``rh_``)."""
+    text = source if isinstance(source, str) and source.lstrip().startswith("<") else Path(source).read_text()
+    root = ET.fromstring(text)
+    if root.tag != "mujoco":
+        raise ValueError("not an MJCF document (root element is not <mujoco>)")
+    ctx = _Ctx(root)
+    wb = root.find("worldbody")
+    roots = [] if wb is None else wb.findall("body")
+    if len(roots) != 1:
+        raise ValueError(f"expected one hand root body under <worldbody>, found {len(roots)}")
+
+    bodies: List[M.Body] = []
+    dofs: List[M.Dof] = []
+    geoms: List[M.Geom] = []
+    body_idx: Dict[str, int] = {}
+    joint_idx: Dict[str, int] = {}
+    root_joint_attrs: Dict[str, str] = {}
+
+    def visit(el: ET.Element, parent: int, cls: str):
+        cls = el.get("childclass", cls)
+        a = ctx.attrs(el, "body", cls)
+        bi = len(bodies)
+        name = _strip(a.get("name", f"body{bi}"), prefix)
+        body_idx[name] = bi
+        pos = tuple(_floats(a.get("pos", "0 0 0")))
+        quat = ctx.frame_quat(a)
+        mass, ipos, iquat, diag = 0.0, (0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0), (0.0, 0.0, 0.0)
+        inertial = el.find("inertial")
+        if inertial is not None:
+            ia = ctx.attrs(inertial, "inertial", cls)
+            mass = float(ia["mass"])
+            ipos = tuple(_floats(ia.get("pos", "0 0 0")))
+            if "diaginertia" in ia:
+                iquat = ctx.frame_quat(ia)
+                diag = tuple(_floats(ia["diaginertia"]))
+            elif "fullinertia" in ia:
+                xx, yy, zz, xy, xz, yz = _floats(ia["fullinertia"])
+                w, V = np.linalg.eigh(np.array([[xx, xy, xz], [xy, yy, yz], [xz, yz, zz]]))
+                if np.linalg.det(V) < 0:
+                    V[:, 0] = -V[:, 0]
+                iquat, diag = _mat_quat(V), tuple(float(x) for x in w)
+            else:
+                raise ValueError(f"body {name!r}: <inertial> needs diaginertia or fullinertia")
+        elif parent >= 0:
+            raise ValueError(f"body {name!r}: no <inertial> (inertia from geoms is not supported)")
+        bodies.append(M.Body(name, parent, pos, quat, mass, ipos, iquat, diag))
+        for j in el.findall("joint"):
+            ja = ctx.attrs(j, "joint", cls)
+            if bi == 0:
+                root_joint_attrs.update(ja)
+            jtype = ja.get("type", "hinge")
+            if jtype not in ("hinge", "slide"):
+                raise ValueError(f"joint {ja.get('name')!r}: type {jtype!r} is not supported (hinge/slide)")
+            if float(ja.get("stiffness", "0")) != 0.0:
+                raise ValueError(f"joint {ja.get('name')!r}: joint stiffness is not supported")
+            kind = 0 if jtype == "hinge" else 1
+            rng = (0.0, 0.0)
+            if ctx.limited(ja, "limited", "range"):
+                lo, hi = _floats(ja["range"])
+                rng = (ctx.angle(lo), ctx.angle(hi)) if kind == 0 else (lo, hi)
+            else:
+                raise ValueError(f"joint {ja.get('name')!r}: unlimited joints are not supported")
+            jname = _strip(ja.get("name", f"joint{len(dofs)}"), prefix)
+            joint_idx[jname] = len(dofs)
+            dofs.append(M.Dof(jname, bi, kind, tuple(_floats(ja.get("axis", "0 0 1"))), rng,
+                              float(ja.get("damping", "0")), float(ja.get("armature", "0"))))
+        for g in el.findall("geom"):
+            ga = ctx.attrs(g, "geom", cls)
+            if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
+                continue  # visual only
+            gtype = ga.get("type", "sphere")
+            if gtype not in ("capsule", "cylinder"):
+                raise ValueError(f"body {name!r}: collider type {gtype!r} is not supported "
+                                 "(capsule/cylinder; the kernel has no mesh or box hand colliders)")
+            size = _floats(ga.get("size", "0"))
+            if "fromto" in ga:
+                ft = np.asarray(_floats(ga["fromto"]), np.float64)
+                p0, p1 = ft[:3], ft[3:]
+                d = p1 - p0
+                half = float(np.linalg.norm(d)) / 2
+                gpos, axis = tuple((p0 + p1) / 2), tuple(d / (2 * half))
+            else:
+                if len(size) < 2:
+                    raise ValueError(f"body {name!r}: capsule needs size='radius half-length'")
+                half = size[1]
+                gpos = tuple(_floats(ga.get("pos", "0 0 0")))
+                axis = tuple(M.quat_to_mat(M.quat_normalize(ctx.frame_quat(ga)))[:, 2])
+            geoms.append(M.Geom(bi, gpos, axis, half, size[0]))
+        for child in el.findall("body"):
+            visit(child, bi, cls)
+
+    visit(roots[0], -1, "main")
+    n_menagerie_joints = len(dofs)
+
+    # forearm DOFs on the root body after its own joints (shadow_hand.py:272-311); they
+    # take the root's joint defaults (armature), damping is set by build_model (critical)
+    arm = float(ctx.attrs(roots[0].find("joint") if roots[0].find("joint") is not None else ET.Element("joint"),
+                          "joint", roots[0].get("childclass", "main")).get("armature", "0"))
+    n_root = sum(1 for d in dofs if d.body == 0)
+    slides = [M.Dof(n, 0, k, ax, rng, 0.0, arm) for (n, k, ax, rng) in FOREARM_DOFS]
+    dofs[n_root:n_root] = slides
+    remap = [i if i < n_root else i + len(slides) for i in range(n_menagerie_joints)]
+    joint_idx = {k: remap[v] for k, v in joint_idx.items()}
+
+    tendons: List[Tuple[int, int]] = []
+    tcoef: List[Tuple[float, float]] = []
+    tendon_idx: Dict[str, int] = {}
+    tel = root.find("tendon")
+    for t in ([] if tel is None else tel.findall("fixed")):
+        js = t.findall("joint")
+        if len(js) != 2:
+            raise ValueError(f"fixed tendon {t.get('name')!r}: exactly two joints are supported")
+        try:
+            pair = tuple(joint_idx[_strip(j.get("joint"), prefix)] for j in js)
+        except KeyError as e:
+            raise ValueError(f"fixed tendon {t.get('name')!r}: unknown joint {e}") from None
+        tendon_idx[_strip(t.get("name", f"tendon{len(tendons)}"), prefix)] = len(tendons)
+        tendons.append(pair)
+        tcoef.append(tuple(float(j.get("coef", "1")) for j in js))
+
+    acts = []
+    ael = root.find("actuator")
+    for a in ([] if ael is None else list(ael)):
+        if a.tag != "position":
+            raise ValueError(f"actuator <{a.tag}> is not supported (position only)")
+        aa = ctx.attrs(a, "position", "main")
+        if "joint" in aa:
+            kind, target = 0, joint_idx.get(_strip(aa["joint"], prefix))
+        elif "tendon" in aa:
+            kind, target = 1, tendon_idx.get(_strip(aa["tendon"], prefix))
+        else:
+            raise ValueError(f"actuator {aa.get('name')!r}: needs joint= or tendon=")
+        if target is None:
+            raise ValueError(f"actuator {aa.get('name')!r}: unknown target")
+        if not ctx.limited(aa, "ctrllimited", "ctrlrange"):
+            raise ValueError(f"actuator {aa.get('name')!r}: ctrlrange is required")
+        cr = tuple(_floats(aa["ctrlrange"]))
+        fr = tuple(_floats(aa["forcerange"])) if ctx.limited(aa, "forcelimited", "forcerange") else None
+        acts.append((kind, target, float(aa.get("kp", "1")), cr, fr))
+    for (n, _, _, rng) in FOREARM_DOFS:
+        acts.append((0, joint_idx.setdefault(n, [d.name for d in dofs].index(n)), M.FOREARM_KP, rng, None))
+
+    excludes = []
+    cel = root.find("contact")
+    for e in ([] if cel is None else cel.findall("exclude")):
+        try:
+            excludes.append((body_idx[_strip(e.get("body1"), prefix)], body_idx[_strip(e.get("body2"), prefix)]))
+        except KeyError as err:
+            raise ValueError(f"<exclude>: unknown body {err}") from None
+
+    sites = []
+    for b in FINGERTIP_BODIES:
+        if b not in body_idx:
+            raise ValueError(f"fingertip body {prefix + b!r} not found")
+        sites.append((body_idx[b], (0.0, 0.0, M.THUMBTIP_OFFSET if b == "thdistal" else M.FINGERTIP_OFFSET)))
+
+    # joints_pos observation order: the model's joints in document order, forearm ones last
+    obs_order = [remap[i] for i in range(n_menagerie_joints)] + [n_root + i for i in range(len(slides))]
+
+    for what, got, want in (("bodies", len(bodies), abi.HAND_NBODY), ("joints", len(dofs), abi.HAND_NDOF),
+                            ("capsule colliders", len(geoms), abi.HAND_NGEOM),
+                            ("actuators", len(acts), abi.HAND_NACT), ("fixed tendons", len(tendons), abi.HAND_NTENDON)):
+        if got != want:
+            raise ValueError(f"hand has {got} {what} (with the forearm DOFs); the kernel ABI needs {want}")
+    return M.HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order, tcoef)
+
+
+# ------------------------------------------------------------------ writer
+def _fmt(v) -> str:
+    return " ".join(repr(float(x)) for x in v)
+
+
+def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
+    """Menagerie-style MJCF of a HandSpec, without its forearm DOFs (``load_hand`` adds them
+    back, as the reference's ``_add_dofs`` does). Joint defaults go through nested classes,
+    finger colliders are written as ``fromto`` capsules and each body gets a visual geom, so
+    that the loader's class, frame and filtering paths are all exercised on a round trip."""
+    root = ET.Element("mujoco", model="right_shadow_hand")
+    ET.SubElement(root, "compiler", angle="radian", autolimits="true")
+    dflt = ET.SubElement(root, "default")
+    hand = ET.SubElement(dflt, "default", {"class": "right_hand"})
+    ET.SubElement(hand, "joint", axis="1 0 0", damping="0.05", armature=repr(spec.dofs[2].armature))
+    ET.SubElement(hand, "position", forcerange="-1 1")
+    wrist = ET.SubElement(hand, "default", {"class": "wrist"})
+    ET.SubElement(wrist, "joint", damping="0.5")
+    ET.SubElement(ET.SubElement(hand, "default", {"class": "plastic_collision"}), "geom", type="capsule",
+                  group="3")
+    ET.SubElement(ET.SubElement(hand, "default", {"class": "plastic_visual"}), "geom", type="mesh",
+                  contype="0", conaffinity="0", group="2")
+
+    names = {i: b.name for i, b in enumerate(spec.bodies)}
+    els: Dict[int, ET.Element] = {}
+    wb = ET.SubElement(root, "worldbody")
+    slide_names = {n for (n, _, _, _) in FOREARM_DOFS}
+    for i, b in enumerate(spec.bodies):
+        parent = wb if b.parent < 0 else els[b.parent]
+        attrs = {"name": prefix + b.name, "pos": _fmt(b.pos), "quat": _fmt(b.quat)}
+        if b.parent < 0:
+            attrs["childclass"] = "right_hand"
+        el = ET.SubElement(parent, "body", attrs)
+        els[i] = el
+        ET.SubElement(el, "inertial", pos=_fmt(b.ipos), quat=_fmt(b.iquat), mass=repr(b.mass),
+                      diaginertia=_fmt(b.diag))
+        for d in spec.dofs:
+            if d.body != i or d.name in slide_names:
+                continue
+            ja = {"name": prefix + d.name, "range": _fmt(d.range)}
+            if d.kind == 1:
+                ja["type"] = "slide"
+            if d.name.startswith("WRJ"):
+                ja["class"] = "wrist"
+                if d.damping != 0.5:
+                    ja["damping"] = repr(d.damping)
+            elif d.damping != 0.05:
+                ja["damping"] = repr(d.damping)
+            if tuple(d.axis) != (1.0, 0.0, 0.0):
+                ja["axis"] = _fmt(d.axis)
+            if d.armature != spec.dofs[2].armature:
+                ja["armature"] = repr(d.armature)
+            ET.SubElement(el, "joint", ja)
+        ET.SubElement(el, "geom", {"class": "plastic_visual", "mesh": b.name})
+        for g in spec.geoms:
+            if g.body != i:
+                continue
+            if b.name.endswith(("proximal", "middle", "distal")) and not b.name.startswith("th"):
+                p, a = np.asarray(g.pos), np.asarray(g.axis) * g.halflen
+                ET.SubElement(el, "geom", {"class": "plastic_collision", "size": repr(g.radius),
+                                           "fromto": _fmt(np.concatenate([p - a, p + a]))})
+            else:
+                ET.SubElement(el, "geom", {"class": "plastic_collision", "size": _fmt((g.radius, g.halflen)),
+                                           "pos": _fmt(g.pos), "quat": _fmt(_quat_from_z(g.axis))})
+    cont = ET.SubElement(root, "contact")
+    for a, b in spec.excludes:
+        ET.SubElement(cont, "exclude", body1=prefix + names[a], body2=prefix + names[b])
+    ten = ET.SubElement(root, "tendon")
+    coefs = spec.tendon_coef or [(1.0, 1.0)] * len(spec.tendons)
+    for t, (d2, d1) in enumerate(spec.tendons):
+        fe = ET.SubElement(ten, "fixed", name=f"{prefix}T{t}")
+        for d, c in ((d2, coefs[t][0]), (d1, coefs[t][1])):
+            ET.SubElement(fe, "joint", joint=prefix + spec.dofs[d].name, coef=repr(c))
+    act = ET.SubElement(root, "actuator")
+    for (kind, target, kp, cr, fr) in spec.acts:
+        if kind == 0 and spec.dofs[target].name in slide_names:
+            continue
+        aa = {"class": "right_hand", "kp": repr(kp), "ctrlrange": _fmt(cr)}
+        if kind == 0:
+            aa["joint"] = prefix + spec.dofs[target].name
+        else:
+            aa["tendon"] = f"{prefix}T{target}"
+        if fr is None:
+            aa["forcelimited"] = "false"
+        elif tuple(fr) != (-1.0, 1.0):
+            aa["forcerange"] = _fmt(fr)
+        ET.SubElement(act, "position", aa)
+    ET.indent(root)
+    return ET.tostring(root, encoding="unicode")

@@ -26,7 +26,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple
+from typing import List, NamedTuple, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -151,6 +151,22 @@ class Geom:
     axis: Tuple[float, float, float]
     halflen: float
     radius: float
+
+
+class HandSpec(NamedTuple):
+    """One (right) hand as build_model consumes it: the authored tree below, or a user MJCF
+    through ``mjcf.load_hand``. Indices are MuJoCo's: bodies in depth-first document order,
+    dofs in body order, geoms = the capsule colliders in body order."""
+
+    bodies: List[Body]
+    dofs: List[Dof]
+    geoms: List[Geom]
+    excludes: List[Tuple[int, int]]            # <contact><exclude> body pairs
+    sites: List[Tuple[int, Tuple[float, float, float]]]  # fingertip sites (body, pos)
+    tendons: List[Tuple[int, int]]             # fixed tendons: (dof, dof)
+    acts: List[tuple]                          # (kind 0 joint / 1 tendon, target, kp, ctrlrange, forcerange|None)
+    obs_order: List[int]                       # joints_pos observation order (dof indices)
+    tendon_coef: Optional[List[Tuple[float, float]]] = None  # None = (1, 1) each
 
 
 ID = (1.0, 0.0, 0.0, 0.0)
@@ -281,7 +297,12 @@ def _right_hand_tree():
     acts = [(k, dof_idx[t] if k == 0 else t, kp, cr, fr) for (k, t, kp, cr, fr) in acts]
     # joints_pos order: Menagerie joints in document order, forearm joints appended last.
     obs_order = list(range(2, abi.HAND_NDOF)) + [0, 1]
-    return bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order
+    return HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order)
+
+
+def authored_hand() -> HandSpec:
+    """The authored right hand (the default of build_model)."""
+    return _right_hand_tree()
 
 
 def _mirror_quat(q):
@@ -318,8 +339,11 @@ def _subtree_mass(bodies, root):
 
 
 def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: float = PHYSICS_TIMESTEP,
-                hand_collisions: bool = True) -> abi.ModelDesc:
+                hand_collisions: bool = True, hand: Optional[HandSpec] = None) -> abi.ModelDesc:
     """Compile the scene into a ``ps_model_desc``.
+
+    ``hand``: the right hand to use (``mjcf.load_hand`` of a user MJCF); default the authored
+    one. The left hand is its mirror image, as for the authored hand.
 
     ``hand_collisions=False`` is ``disable_hand_collisions`` (piano_with_shadow_hands.py:476-489):
     every hand collider gets contype=1, conaffinity=0, so no hand geom pair collides
@@ -353,7 +377,9 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
     m.hand_contact.solimp[:] = (0.5, 0.99, 0.0001, 0.5, 2.0)
     m.hand_contact.friction = 1.0
 
-    bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order = _right_hand_tree()
+    spec = hand if hand is not None else _right_hand_tree()
+    bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order = spec[:8]
+    tcoef = spec.tendon_coef or [(1.0, 1.0)] * len(tendons)
     forearm_mass = _subtree_mass(bodies, 0)
     root_quat = tuple(quat_normalize(HAND_QUAT))
     m.root_geom_count = sum(1 for g in geoms if g.body == 0)
@@ -400,7 +426,7 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
             m.site_pos[h][s][:] = _mirror_vec(pos) if mir else pos
         for t, (d2, d1) in enumerate(tendons):
             m.tendon_dof[h][t][:] = (d2, d1)
-            m.tendon_coef[h][t][:] = (1.0, 1.0)
+            m.tendon_coef[h][t][:] = tcoef[t]
         for a, (kind, target, kp, cr, fr) in enumerate(acts):
             m.act_kind[h][a] = kind
             m.act_target[h][a] = target

@@ -1,0 +1,138 @@
+"""MJCF-subset hand loader (diffusion-piano_amd/mjcf.py).
+
+The Menagerie Shadow Hand XML the reference loads (shadow_hand.py:93-125) is not in the
+container, so the loader is pinned by round trips of the authored hand through
+``hand_to_mjcf`` (classes, fromto capsules, visual geoms, tendons, excludes). Hand-written
+snippets cover each MJCF rule used: degree/radian, euler sequences, class inheritance,
+childclass, collider filtering, cylinder -> capsule, fullinertia, and the errors.
+"""
+import importlib
+import math
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def mj():
+    return importlib.import_module("diffusion-piano_amd.mjcf")
+
+
+def _desc_arrays(m):
+    out = {}
+    for name, _ in m._fields_:
+        v = getattr(m, name)
+        if hasattr(v, "_length_"):
+            out[name] = np.ctypeslib.as_array(v).astype(np.float64)
+        elif hasattr(v, "_fields_"):
+            out.update({f"{name}.{k}": np.asarray(getattr(v, k), np.float64).ravel() for k, _ in v._fields_})
+        else:
+            out[name] = np.float64(v)
+    return out
+
+
+def test_round_trip_equals_authored_model(dp, mj):
+    xml = mj.hand_to_mjcf(dp.model.authored_hand())
+    assert xml.count("<body ") == 25 and "fromto" in xml and 'contype="0"' in xml
+    a = _desc_arrays(dp.model.build_model())
+    b = _desc_arrays(dp.model.build_model(hand=mj.load_hand(xml)))
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=0, atol=1e-12, err_msg=k)
+
+
+def test_round_trip_of_loaded_spec_is_a_fixed_point(dp, mj):
+    s1 = mj.load_hand(mj.hand_to_mjcf(dp.model.authored_hand()))
+    s2 = mj.load_hand(mj.hand_to_mjcf(s1))
+    assert [b.name for b in s1.bodies] == [b.name for b in s2.bodies]
+    assert s1.obs_order == s2.obs_order and s1.tendons == s2.tendons and s1.excludes == s2.excludes
+    assert [a[:3] for a in s1.acts] == [a[:3] for a in s2.acts]
+
+
+def test_task_config_hand_xml(dp, mj, tmp_path):
+    path = tmp_path / "right_hand.xml"
+    path.write_text(mj.hand_to_mjcf(dp.model.authored_hand()))
+    seq = dp.music.twinkle_twinkle_little_star_one_hand()
+    md_a, _, _ = dp.compile_task(seq, dp.TaskConfig())
+    md_b, _, _ = dp.compile_task(seq, dp.TaskConfig(hand_xml=str(path)))
+    a, b = _desc_arrays(md_a), _desc_arrays(md_b)
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=0, atol=1e-12, err_msg=k)
+
+
+def _edit(xml, old, new):
+    assert old in xml, old
+    return xml.replace(old, new, 1)
+
+
+@pytest.fixture(scope="module")
+def base_xml(dp, mj):
+    return mj.hand_to_mjcf(dp.model.authored_hand())
+
+
+def test_degrees_and_euler(dp, mj, base_xml):
+    """compiler angle=degree converts hinge ranges and euler angles (slides untouched);
+    euler 'xyz' composes rotating-axis rotations."""
+    xml = _edit(base_xml, 'angle="radian"', 'angle="degree"')
+    xml = _edit(xml, 'name="rh_WRJ2" range="-0.523599 0.174533"', 'name="rh_WRJ2" range="-30 10"')
+    xml = _edit(xml, 'name="rh_palm" pos="0.0 0.0 0.034" quat="1.0 0.0 0.0 0.0"',
+                'name="rh_palm" pos="0.0 0.0 0.034" euler="90 0 90"')
+    spec = mj.load_hand(xml)
+    wr = [d for d in spec.dofs if d.name == "WRJ2"][0]
+    assert wr.range == pytest.approx((math.radians(-30), math.radians(10)))
+    palm = [b for b in spec.bodies if b.name == "palm"][0]
+    q = palm.quat  # Rx(90) then Rz(90) about the rotated z
+    R = dp.model.quat_to_mat(q)
+    Rx = dp.model.quat_to_mat((math.cos(math.pi / 4), math.sin(math.pi / 4), 0, 0))
+    Rz = dp.model.quat_to_mat((math.cos(math.pi / 4), 0, 0, math.sin(math.pi / 4)))
+    np.testing.assert_allclose(R, Rx @ Rz, atol=1e-12)
+    ty = [d for d in spec.dofs if d.name == "forearm_ty"][0]
+    assert ty.range == dp.model.FOREARM_TY_RANGE
+
+
+def test_class_inheritance_and_overrides(mj, base_xml):
+    xml = _edit(base_xml, '<joint damping="0.5" />', '<joint damping="0.7" armature="0.001" />')
+    spec = mj.load_hand(xml)
+    by = {d.name: d for d in spec.dofs}
+    assert by["WRJ1"].damping == 0.7 and by["WRJ1"].armature == 0.001   # class wrist
+    assert by["FFJ3"].damping == 0.05 and by["FFJ3"].armature == 0.0002  # parent class right_hand
+    assert by["forearm_tx"].armature == 0.0002                           # root childclass defaults
+
+
+def test_cylinder_collider_becomes_capsule_and_visuals_are_skipped(mj, base_xml):
+    xml = _edit(base_xml, '<geom class="plastic_collision" size="0.035 0.06"',
+                '<geom class="plastic_collision" type="cylinder" size="0.035 0.06"')
+    spec = mj.load_hand(xml)
+    assert spec.geoms[0].radius == 0.035 and spec.geoms[0].halflen == 0.06
+    xml = _edit(base_xml, '<geom class="plastic_visual" mesh="forearm" />',
+                '<geom class="plastic_visual" mesh="forearm" contype="1" />')
+    with pytest.raises(ValueError, match="collider type 'mesh'"):
+        mj.load_hand(xml)
+
+
+def test_fullinertia_matches_diaginertia(dp, mj, base_xml):
+    spec = mj.load_hand(base_xml)
+    wrist = [b for b in spec.bodies if b.name == "wrist"][0]
+    I = dp.model.quat_to_mat(wrist.iquat) @ np.diag(wrist.diag) @ dp.model.quat_to_mat(wrist.iquat).T
+    full = " ".join(repr(float(x)) for x in (I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]))
+    xml = _edit(base_xml, 'quat="0.5 0.5 0.5 0.5" mass="0.1" diaginertia="6.4e-05 4.38e-05 3.5e-05"',
+                f'mass="0.1" fullinertia="{full}"')
+    w2 = [b for b in mj.load_hand(xml).bodies if b.name == "wrist"][0]
+    I2 = dp.model.quat_to_mat(w2.iquat) @ np.diag(w2.diag) @ dp.model.quat_to_mat(w2.iquat).T
+    np.testing.assert_allclose(I2, I, atol=1e-18)
+
+
+def test_errors(mj, base_xml):
+    with pytest.raises(ValueError, match="not an MJCF"):
+        mj.load_hand("<robot/>")
+    with pytest.raises(ValueError, match="capsule colliders"):
+        mj.load_hand(_edit(base_xml, '<geom class="plastic_collision" size="0.035 0.06" pos="0.0 0.0 0.11" '
+                                     'quat="1.0 0.0 0.0 0.0" />', ""))
+    with pytest.raises(ValueError, match="unknown default class"):
+        mj.load_hand(_edit(base_xml, 'class="wrist"', 'class="nope"'))
+    with pytest.raises(ValueError, match="stiffness"):
+        mj.load_hand(_edit(base_xml, 'name="rh_WRJ2"', 'name="rh_WRJ2" stiffness="3"'))
+    with pytest.raises(ValueError, match="ball"):
+        mj.load_hand(_edit(base_xml, 'name="rh_WRJ2"', 'name="rh_WRJ2" type="ball"'))
+    with pytest.raises(ValueError, match="unknown joint"):
+        mj.load_hand(_edit(base_xml, 'joint="rh_FFJ2" coef', 'joint="rh_XXJ2" coef'))
