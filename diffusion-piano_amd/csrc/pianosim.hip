@@ -272,7 +272,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
   for (int g = 0; g < NDT; g++) {
     int p[2] = {0, 0};
     for (int a = 1; a < MAXDEP; a++) {
-      int v = a <= m->dof_depth[g] ? m->dof_anc[g][a] : 255;
+      int v = a <= m->dof_depth[g] ? m->dof_anc[g][a] : g;  // past the root: the dof itself (a valid lane)
       p[(a - 1) / 4] |= v << (8 * ((a - 1) % 4));
     }
     m->dof_anc_pack[g][0] = p[0];
