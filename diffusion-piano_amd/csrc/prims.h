@@ -261,8 +261,13 @@ __device__ __forceinline__ float seg_box_t(f3 a3, f3 d3, const float* hs) {
 // Not inlined: its four call sites (count / write pass, substep / task layer) would each
 // carry a copy of the segment-box search, and the kernel is instruction-cache bound enough
 // that one shared copy measures ~2% faster (tools/throughput.py A/B on MI355X).
-__device__ __noinline__ int capsule_box(f3 p0, f3 p1, float r, f3 c, const float* R, const float* hs, Contact* out, int slot,
+// The box frame is a rotation about +y (keys; the base: cq = 1, sq = 0) and comes in by
+// value, like the half sizes: arrays passed by pointer to an out-of-line function live in
+// scratch memory, a store/load round trip through the vector memory path per call.
+__device__ __noinline__ int capsule_box(f3 p0, f3 p1, float r, f3 c, float cq, float sq, f3 hsv, Contact* out, int slot,
                            int maxc, int kind, int key, int g2) {
+  const float R[9] = {cq, 0.f, sq, 0.f, 1.f, 0.f, -sq, 0.f, cq};
+  const float hs[3] = {hsv.x, hsv.y, hsv.z};
   int n = 0;
   f3 nrm, pos;
   for (int e = 0; e < 2; e++) {
