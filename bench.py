@@ -132,7 +132,7 @@ def issue_summary(n_envs, song):
     counter pass (tools/collect_pmc.py): fractions of the waves' lifetime issuing / waiting."""
     d = _profile("pmc_latest.json")
     if d and d.get("envs") == n_envs and d.get("song", song) == song and "wave_issue_frac" in d:
-        return {k: d[k] for k in ("wave_issue_frac", "wave_wait_frac", "wave_ifetch_frac", "valu_insts_per_env_step")}
+        return {k: d[k] for k in ("wave_issue_frac", "wave_wait_frac", "wave_issue_stall_frac", "valu_insts_per_env_step")}
     return None
 
 

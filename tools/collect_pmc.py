@@ -5,7 +5,8 @@ usage: python tools/collect_pmc.py <trace_dir> <fetch_dir> <write_dir> <envs> <s
 * <trace_dir>: `rocprofv3 --kernel-trace --stats --output-format csv` of bench.py
 * <fetch_dir>/<write_dir>: separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes
 * [sq_dir]: a `--pmc` pass of the SQ wave-state counters (SQ_COUNTERS below): how much of
-  the waves' lifetime issues an instruction vs waits on a counter / instruction fetch
+  the waves' lifetime issues an instruction vs waits on a counter (s_waitcnt / barrier) vs
+  is stalled at issue (dependency or pipe busy: SQ_WAIT_INST_ANY, MI355X_MICROARCH.md)
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md, HBM:
 FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950; units KB).
 """
@@ -70,7 +71,7 @@ def main():
             wc = sq["SQ_WAVE_CYCLES"]
             out["wave_issue_frac"] = sq["SQ_ACTIVE_INST_ANY"] / wc  # lifetime issuing
             out["wave_wait_frac"] = sq["SQ_WAIT_ANY"] / wc  # waiting on s_waitcnt
-            out["wave_ifetch_frac"] = sq["SQ_WAIT_INST_ANY"] / wc  # waiting on instruction fetch
+            out["wave_issue_stall_frac"] = sq["SQ_WAIT_INST_ANY"] / wc  # issue stalls (RAW dependency / pipe)
             out["valu_insts_per_env_step"] = sq["SQ_INSTS_VALU"] / envs
     Path("profiles").mkdir(exist_ok=True)
     if stats:
