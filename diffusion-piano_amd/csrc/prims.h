@@ -373,24 +373,30 @@ __device__ __forceinline__ float tolerance(float x, float lo, float hi, float ma
   return expf(-0.5f * dd * dd * scale2);
 }
 
-// rectangular min-cost assignment (rows n <= cols mm), sum of tol over assigned pairs
-__device__ float hungarian_tol(int n, int mm, const float* c /*[n][mm]*/) {
-  float u[17], v[17], minv[17];
-  int p[17], way[17];
-  bool used[17];
+// rectangular min-cost assignment (rows n <= cols mm), sum of tol over assigned pairs.
+// Runs on one lane; its work arrays (w: 3 * (mm + 1) floats then 3 * (mm + 1) ints) are in
+// LDS: as private arrays with data-dependent indices they would sit in scratch memory.
+__device__ __forceinline__ float hungarian_tol(int n, int mm, const float* c /*[n][mm]*/, float* w) {
+  float* u = w;
+  float* v = u + (mm + 1);
+  float* minv = v + (mm + 1);
+  int* p = reinterpret_cast<int*>(minv + (mm + 1));
+  int* way = p + (mm + 1);
+  int* used = way + (mm + 1);
   for (int i = 0; i <= n; i++) u[i] = 0.f;
   for (int j = 0; j <= mm; j++) { v[j] = 0.f; p[j] = 0; way[j] = 0; }
   for (int i = 1; i <= n; i++) {
     p[0] = i;
     int j0 = 0;
-    for (int j = 0; j <= mm; j++) { minv[j] = INFINITY; used[j] = false; }
+    for (int j = 0; j <= mm; j++) { minv[j] = INFINITY; used[j] = 0; }
     do {
-      used[j0] = true;
+      used[j0] = 1;
       int i0 = p[j0], j1 = 0;
       float delta = INFINITY;
+      const float ui0 = u[i0];
       for (int j = 1; j <= mm; j++)
         if (!used[j]) {
-          float cur = c[(i0 - 1) * mm + j - 1] - u[i0] - v[j];
+          float cur = c[(i0 - 1) * mm + j - 1] - ui0 - v[j];
           if (cur < minv[j]) { minv[j] = cur; way[j] = j0; }
           if (minv[j] < delta) { delta = minv[j]; j1 = j; }
         }
