@@ -176,6 +176,8 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       p = m->body_parent[p];
     }
     dpar[g] = par;
+    // the kernel's chain-row L^-T (row_LT_chain) relies on ancestors having lower indices
+    if (par >= g) return fail("dofs are not in tree order");
   }
   int maxdep = 0;
   for (int g = 0; g < NDT; g++) {
