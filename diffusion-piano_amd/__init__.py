@@ -10,3 +10,4 @@ from .envs import (  # noqa: F401
     VectorizedPianoEnv, compile_task, load, obs_layout,
 )
 from .evaluation import MidiEvaluationWrapper  # noqa: F401,E402
+from ._lib import PianosimError  # noqa: F401,E402

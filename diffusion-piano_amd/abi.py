@@ -18,6 +18,7 @@ MAX_NOTES = 16
 MAX_CONTACTS_LIMIT = 24
 MAX_ROWS = 64
 NTERMS = 5
+NSTATS = 4  # ps_solver_stats slots: solves, contact-cap substeps, row-cap substeps, max rows requested
 NMUSIC = 6  # ps_musical_metrics slots: precision, recall, f1, sustain_precision, sustain_recall, sustain_f1
 FIRST, MID, LAST = 0, 1, 2
 
@@ -96,7 +97,12 @@ class SongDesc(C.Structure):
 class TaskCfg(C.Structure):
     _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
                 ("wrong_press_termination", i32), ("energy_penalty_coef", d),
-                ("pgs_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32)]
+                ("pgs_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32),
+                ("solver", i32), ("randomize_hand_positions", i32)]
+
+
+SOLVER_PGS, SOLVER_EXACT = 0, 1
+HAND_POSITION_OFFSET = 0.05  # piano_with_shadow_hands.py:46
 
 
 def obs_dim(cfg: TaskCfg) -> int:

@@ -49,6 +49,10 @@ struct ps_env {
   bool ordered;
   uint8_t* last;
   bool applied_on;
+  float* hand_dy;           // randomize_hand_positions: this episode's y shift of both hands
+  int* episode;             // resets so far per env (the draw counter)
+  int* stats;               // [N][PS_NSTATS] solver / cap counters of the last step
+  uint64_t seed;
 };
 
 static void quat2mat_h(const double* q, float* R) {
@@ -353,15 +357,23 @@ int ps_obs_dim(const ps_task_cfg* cfg) {
 
 int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_task_cfg* cfg, int n_envs, int device,
               uint64_t seed, ps_env** out) {
-  (void)seed;
   if (!model || !song || !cfg || !out) return fail("null argument");
   if (n_envs <= 0) return fail("n_envs must be positive");
   if (song->T <= 0) return fail("empty song");
   if (cfg->n_steps_lookahead < 0) return fail("negative lookahead");
   if (cfg->max_contacts < 0 || cfg->max_contacts > MAXCON) return fail("max_contacts out of range");
   if (cfg->pgs_iterations < 0) return fail("negative pgs_iterations");
-  for (int t = 0; t < song->T; t++)
+  if (cfg->solver != PS_SOLVER_PGS && cfg->solver != PS_SOLVER_EXACT) return fail("unknown solver");
+  for (int t = 0; t < song->T; t++) {
     if (song->count[t] < 0 || song->count[t] > PS_MAX_NOTES) return fail("bad note count");
+    // the ot_fingering reward assigns the step's goal keys to fingertips in a table of
+    // PS_MAX_NOTES columns (piano_with_shadow_hands.py:340-361 has no cap): more is an error
+    int k = 0;
+    for (int j = 0; j < NK; j++) k += song->goal[(size_t)t * (NK + 1) + j] != 0.f;
+    if (k > PS_MAX_NOTES)
+      return fail("step " + std::to_string(t) + " has " + std::to_string(k) + " goal keys; at most " +
+                  std::to_string(PS_MAX_NOTES) + " are supported");
+  }
   HIPCHK(hipSetDevice(device));
   DevModel* hm = new DevModel;
   if (build_dev_model(model, hm)) { delete hm; return -1; }
@@ -398,6 +410,13 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMalloc(&E->mus_cnt, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->order, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->last, N));
+  HIPCHK(hipMalloc(&E->hand_dy, sizeof(float) * N));
+  HIPCHK(hipMalloc(&E->episode, sizeof(int) * N));
+  HIPCHK(hipMalloc(&E->stats, sizeof(int) * N * PS_NSTATS));
+  HIPCHK(hipMemset(E->hand_dy, 0, sizeof(float) * N));
+  HIPCHK(hipMemset(E->episode, 0, sizeof(int) * N));
+  HIPCHK(hipMemset(E->stats, 0, sizeof(int) * N * PS_NSTATS));
+  E->seed = seed;
   HIPCHK(hipMemset(E->qpos, 0, sizeof(float) * N * NV));
   HIPCHK(hipMemset(E->qvel, 0, sizeof(float) * N * NV));
   HIPCHK(hipMemset(E->qws, 0, sizeof(float) * N * NV));
@@ -426,37 +445,40 @@ void ps_destroy(ps_env* E) {
   hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
   hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
+  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats);
   delete E;
 }
 
-// Dispatch order of a step launch: envs by their last contact count, descending, envs about
-// to auto-reset (no physics this step) last. Workgroups are dispatched in blockIdx order, so
-// the expensive envs start in the first wave of workgroups and the cheap ones fill the slots
-// freed late (longest-processing-time-first): the launch's tail is shorter. Each env's
-// result is independent of the order.
+// Dispatch order of a step launch: envs by the cost of their previous step, descending -
+// the most coupled constraint rows one of its substeps requested (PS_STAT_MAX_ROWS: the
+// constraint phases and the exact solve grow with it) - envs about to auto-reset (no physics
+// this step) last. Workgroups are dispatched in blockIdx order, so the expensive envs start in
+// the first wave of workgroups and the cheap ones fill the slots freed late (longest-
+// processing-time-first): the launch's tail is shorter. Each env's result is independent of
+// the order.
 constexpr int ORDER_THREADS = 1024;
-__global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restrict__ ncon,
+constexpr int ORDER_BUCKETS = 66;  // 0: resets, 1 + min(rows, 64)
+__global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restrict__ stats,
                                                               const uint8_t* __restrict__ last,
                                                               int* __restrict__ order, int n) {
-  constexpr int NB = MAXCON + 2;  // bucket 0: resets, 1 + c: c contacts
-  __shared__ int hist[NB], base[NB];
-  if (threadIdx.x < NB) hist[threadIdx.x] = 0;
+  __shared__ int hist[ORDER_BUCKETS], base[ORDER_BUCKETS];
+  if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
   __syncthreads();
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int b = last[e] ? 0 : 1 + min(max(ncon[e], 0), MAXCON);
+    const int b = last[e] ? 0 : 1 + min(max(stats[(size_t)e * PS_NSTATS + PS_STAT_MAX_ROWS], 0), 64);
     atomicAdd(&hist[b], 1);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
-    for (int b = NB - 1; b >= 0; b--) {  // most contacts first, resets last
+    for (int b = ORDER_BUCKETS - 1; b >= 0; b--) {  // most rows first, resets last
       base[b] = acc;
       acc += hist[b];
     }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int b = last[e] ? 0 : 1 + min(max(ncon[e], 0), MAXCON);
+    const int b = last[e] ? 0 : 1 + min(max(stats[(size_t)e * PS_NSTATS + PS_STAT_MAX_ROWS], 0), 64);
     order[atomicAdd(&base[b], 1)] = e;
   }
 }
@@ -466,13 +488,14 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
   Song song{E->T, E->d_goal, E->d_count, E->d_keys, E->d_fingers};
   Cfg cfg{E->cfg.n_steps_lookahead, E->cfg.fingering_reward, E->cfg.forearm_reward, E->cfg.wrong_press_termination,
           E->cfg.pgs_iterations, E->cfg.max_contacts, E->obs_dim, E->cfg.canonical_actions,
-          (float)E->cfg.energy_penalty_coef, 0};
-  if (const char* sk = getenv("PIANOSIM_SKIP")) cfg.skip = atoi(sk);
+          (float)E->cfg.energy_penalty_coef, E->cfg.solver == PS_SOLVER_EXACT, E->cfg.randomize_hand_positions != 0,
+          (uint32_t)E->seed, (uint32_t)(E->seed >> 32)};
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
-         E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt};
+         E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt,
+         E->hand_dy, E->episode, E->stats};
   const int* order = nullptr;
   if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
-    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->ncon, E->last, E->order,
+    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->stats, E->last, E->order,
                        E->n);
     HIPCHK(hipGetLastError());
     order = E->order;
@@ -578,6 +601,27 @@ int ps_musical_metrics(ps_env* E, float* episode, int32_t* episodes, void* strea
                           (hipStream_t)stream));
   if (episodes)
     HIPCHK(hipMemcpyAsync(episodes, E->mus_cnt, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+int ps_solver_stats(ps_env* E, int32_t* stats, void* stream) {
+  if (!E || !stats) return fail("null argument");
+  HIPCHK(hipMemcpyAsync(stats, E->stats, sizeof(int) * E->n * PS_NSTATS, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+int ps_get_hand_offset(ps_env* E, float* dy, int32_t* episodes, void* stream) {
+  if (!E) return fail("null argument");
+  if (dy) HIPCHK(hipMemcpyAsync(dy, E->hand_dy, sizeof(float) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  if (episodes)
+    HIPCHK(hipMemcpyAsync(episodes, E->episode, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+int ps_set_hand_offset(ps_env* E, const float* dy, void* stream) {
+  if (!E || !dy) return fail("null argument");
+  if (!E->cfg.randomize_hand_positions) return fail("ps_set_hand_offset needs randomize_hand_positions");
+  HIPCHK(hipMemcpyAsync(E->hand_dy, dy, sizeof(float) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }
 

@@ -134,6 +134,27 @@ __device__ __forceinline__ void wsync() {
   asm volatile("" ::: "memory");
 }
 
+// Philox4x32-10 (Salmon et al., SC'11), 10 rounds
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+// randomize_hand_positions draw of (seed, env, episode): U(-0.05, 0.05) from 24 random bits,
+// as oracle/pianosim_ref.c ref_hand_offset_draw (bitwise: same bits, same fma)
+__device__ __forceinline__ float hand_offset_draw(uint32_t seed_lo, uint32_t seed_hi, int env, int episode) {
+  uint32_t c[4] = {(uint32_t)episode, (uint32_t)env, 0x68616e64u /* "hand" */, 0u};
+  philox4x32_10(c, seed_lo, seed_hi);
+  const float u = (float)(c[0] >> 8) * 0x1p-24f;
+  return fmaf((float)(2.0 * PS_HAND_POSITION_OFFSET), u, (float)-PS_HAND_POSITION_OFFSET);
+}
+
 struct Contact {
   float pos[3], n[3], t1[3], t2[3], dist;
   int kind, key, g1, g2;  // g1: -1 for key/base (kind 0/1)

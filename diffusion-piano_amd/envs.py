@@ -93,9 +93,14 @@ class TaskConfig:
     disable_colorization: bool = False  # rendering only: no effect here
     disable_hand_collisions: bool = False
     energy_penalty_coef: float = 5e-3
+    randomize_hand_positions: bool = False  # piano_with_shadow_hands.py:64,491-499
     control_timestep: float = model_lib.CONTROL_TIMESTEP
     physics_timestep: float = model_lib.PHYSICS_TIMESTEP
-    pgs_iterations: int = 20
+    # Constraint solve: "exact" = the solution of the dual problem (what MuJoCo's solvers
+    # converge to), after `pgs_iterations` warm-up sweeps; "pgs" = `pgs_iterations` cold-start
+    # projected Gauss-Seidel sweeps only (truncated, the round-1 solver).
+    constraint_solver: str = "exact"
+    pgs_iterations: Optional[int] = None  # None: 8 warm-up sweeps (exact) / 20 sweeps (pgs)
     max_contacts: int = 20
     hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
 
@@ -135,7 +140,12 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
     tc.forearm_reward = int(not cfg.disable_forearm_reward)
     tc.wrong_press_termination = int(cfg.wrong_press_termination)
     tc.energy_penalty_coef = cfg.energy_penalty_coef
-    tc.pgs_iterations = cfg.pgs_iterations
+    if cfg.constraint_solver not in ("exact", "pgs"):
+        raise ValueError(f"constraint_solver must be 'exact' or 'pgs', got {cfg.constraint_solver!r}")
+    tc.solver = abi.SOLVER_EXACT if cfg.constraint_solver == "exact" else abi.SOLVER_PGS
+    tc.pgs_iterations = cfg.pgs_iterations if cfg.pgs_iterations is not None else (
+        8 if cfg.constraint_solver == "exact" else 20)
+    tc.randomize_hand_positions = int(cfg.randomize_hand_positions)
     tc.max_contacts = min(cfg.max_contacts, abi.MAX_CONTACTS_LIMIT)
     tc.canonical_actions = int(canonical_actions)
     return md, song, tc
@@ -289,6 +299,27 @@ class BatchedPianoEnv:
         _lib.check(_lib.load().ps_musical_metrics(self._h, ep.data_ptr(), cnt.data_ptr(), self.stream))
         return ep, cnt
 
+    def solver_stats(self):
+        """[N, 4] int32 counters of each env's last step: exact-solve linear solves, substeps at
+        the contact cap, substeps that dropped rows past PS_MAX_ROWS, most rows requested."""
+        t = self._torch.empty(self.num_envs, abi.NSTATS, device=self.device, dtype=self._torch.int32)
+        _lib.check(_lib.load().ps_solver_stats(self._h, t.data_ptr(), self.stream))
+        return t
+
+    def hand_offset(self):
+        """-> (dy [N] f32, episodes [N] i32): randomize_hand_positions' y shift of both hands this
+        episode (piano_with_shadow_hands.py:491-499) and each env's resets so far."""
+        torch = self._torch
+        dy = torch.empty(self.num_envs, device=self.device)
+        ep = torch.empty(self.num_envs, device=self.device, dtype=torch.int32)
+        _lib.check(_lib.load().ps_get_hand_offset(self._h, dy.data_ptr(), ep.data_ptr(), self.stream))
+        return dy, ep
+
+    def set_hand_offset(self, dy):
+        t = self._torch.as_tensor(dy, device=self.device, dtype=self._torch.float32).contiguous()
+        _lib.check(_lib.load().ps_set_hand_offset(self._h, t.data_ptr(), self.stream))
+        self._dy = t
+
     def obs_dict(self, obs=None) -> Dict[str, Any]:
         obs = self.obs if obs is None else obs
         return {k: obs[:, s] for k, s in self.obs_slices.items()}
@@ -329,13 +360,14 @@ class VectorizedPianoEnv:
     the reference hard-codes (parallelized_base_v2.py:28-39).
     """
 
-    def __init__(self, num_envs: int, midi_sequence, return_numpy: bool = False, device=None, **task_kwargs):
+    def __init__(self, num_envs: int, midi_sequence, return_numpy: bool = False, device=None, seed: int = 0,
+                 **task_kwargs):
         kw = dict(n_steps_lookahead=1, trim_silence=True, wrong_press_termination=False,
                   initial_buffer_time=0.0, disable_fingering_reward=False, disable_forearm_reward=False,
                   disable_colorization=False, disable_hand_collisions=False)
         kw.update(task_kwargs)
         self.num_envs = num_envs
-        self._core = BatchedPianoEnv(num_envs, midi_sequence, TaskConfig(**kw), device=device)
+        self._core = BatchedPianoEnv(num_envs, midi_sequence, TaskConfig(**kw), device=device, seed=seed)
         self.return_numpy = return_numpy
         self.envs = [_EnvView(self, i) for i in range(num_envs)]
         self.observation_spec = self._core.observation_spec()
@@ -345,29 +377,33 @@ class VectorizedPianoEnv:
     def core(self) -> BatchedPianoEnv:
         return self._core
 
-    def _out(self, x):
+    def _obs(self, obs):
+        # The reference returns fresh arrays each call (parallelized_base_v2.py:60-67); the
+        # core's obs / reward buffers are reused by the next step, so the torch mode returns a
+        # copy (one [N, obs_dim] device copy per step) that a driver may keep across steps.
         if self.return_numpy:
-            return x.detach().cpu().numpy().astype(np.float64)
-        return x
+            flat = obs.detach().cpu().numpy().astype(np.float64)
+        else:
+            flat = obs.clone()
+        return {k: flat[:, s] for k, s in self._core.obs_slices.items()}
 
     def reset(self):
-        obs = self._core.reset()
-        return {k: self._out(v) for k, v in self._core.obs_dict(obs).items()}
+        return self._obs(self._core.reset())
 
     def step(self, actions):
         obs, rew, disc, st = self._core.step(actions)
-        obs_d = {k: self._out(v) for k, v in self._core.obs_dict(obs).items()}
+        obs_d = self._obs(obs)
         dones = st == abi.LAST
         if self.return_numpy:
             return obs_d, rew.detach().cpu().numpy().astype(np.float64), dones.cpu().numpy()
-        return obs_d, rew, dones
+        return obs_d, rew.clone(), dones
 
 
 class Environment:
     """Single-env dm_env facade (``composer_utils.Environment`` + ``CanonicalSpecWrapper``)."""
 
-    def __init__(self, midi, task: Optional[TaskConfig] = None, device=None):
-        self._core = BatchedPianoEnv(1, midi, task, device=device)
+    def __init__(self, midi, task: Optional[TaskConfig] = None, device=None, seed: int = 0):
+        self._core = BatchedPianoEnv(1, midi, task, device=device, seed=seed)
 
     def reset(self) -> TimeStep:
         obs = self._core.reset()
@@ -408,4 +444,5 @@ def song_for(environment_name: str, midi_file=None) -> music.NoteSequence:
 
 def load(environment_name: str, midi_file=None, seed=None, task_kwargs=None, device=None) -> Environment:
     """``robopianist.suite.load`` (suite/__init__.py:50-93) for the debug songs / MIDI files."""
-    return Environment(song_for(environment_name, midi_file), TaskConfig(**(task_kwargs or {})), device=device)
+    return Environment(song_for(environment_name, midi_file), TaskConfig(**(task_kwargs or {})), device=device,
+                       seed=0 if seed is None else int(seed))

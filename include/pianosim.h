@@ -150,11 +150,22 @@ typedef struct {
   int32_t forearm_reward;           /* 1: add forearm reward term */
   int32_t wrong_press_termination;
   double energy_penalty_coef;       /* 5e-3 */
-  int32_t pgs_iterations;           /* constraint solver sweeps per substep */
+  int32_t pgs_iterations;           /* PGS sweeps per substep: the whole solve (PS_SOLVER_PGS) or
+                                       the warm-up of the exact solve (PS_SOLVER_EXACT) */
   int32_t max_contacts;             /* per env, <= PS_MAX_CONTACTS_LIMIT */
   int32_t canonical_actions;        /* 1: ps_step actions are in [-1,1] and are rescaled to the
                                        spec as dm_env_wrappers.CanonicalSpecWrapper does */
+  int32_t solver;                   /* PS_SOLVER_EXACT (default) or PS_SOLVER_PGS */
+  int32_t randomize_hand_positions; /* piano_with_shadow_hands.py:64,491-499: each episode shifts
+                                       both hands by the same U(-0.05, 0.05) m along y */
 } ps_task_cfg;
+
+/* Constraint solvers. EXACT: the solution of the coupled rows' dual problem (block principal
+ * pivoting over LDL' solves after pgs_iterations warm-up sweeps) = what MuJoCo's solvers
+ * converge to. PGS: pgs_iterations cold-start projected Gauss-Seidel sweeps, truncated. */
+#define PS_SOLVER_PGS 0
+#define PS_SOLVER_EXACT 1
+#define PS_HAND_POSITION_OFFSET 0.05  /* piano_with_shadow_hands.py:46 _POSITION_OFFSET */
 
 #define PS_MAX_CONTACTS_LIMIT 24
 /* Coupled constraint rows per env (hand limits, contacted-key limits, 4 per contact);
@@ -182,6 +193,13 @@ typedef struct {
 #define PS_MUS_SUSTAIN_RECALL 4
 #define PS_MUS_SUSTAIN_F1 5
 #define PS_NMUSIC 6
+
+/* Slots of ps_solver_stats: per env, over the substeps of its last step. */
+#define PS_STAT_SOLVES 0        /* linear solves of the exact dual solve (summed) */
+#define PS_STAT_CONTACT_CAP 1   /* substeps whose narrow phase found >= max_contacts contacts */
+#define PS_STAT_ROW_CAP 2       /* substeps that dropped coupled rows past PS_MAX_ROWS */
+#define PS_STAT_MAX_ROWS 3      /* most coupled rows requested in one substep */
+#define PS_NSTATS 4
 
 typedef struct ps_env ps_env;
 
@@ -225,6 +243,16 @@ int ps_contact_count(ps_env* env, int32_t* ncon, void* stream);
  * in evaluation.py:114-177, averaged over the episode's steps), and the number of episodes
  * each env has finished since ps_create, [N]. Device pointers; either may be NULL. */
 int ps_musical_metrics(ps_env* env, float* episode, int32_t* episodes, void* stream);
+
+/* Solver / cap counters of each env's last step, [N][PS_NSTATS] int32 (device). No reference
+ * counterpart: the evidence that the contact and row caps do not bind. */
+int ps_solver_stats(ps_env* env, int32_t* stats, void* stream);
+
+/* randomize_hand_positions (piano_with_shadow_hands.py:491-499): each env's current y shift of
+ * both hand roots [N] f32 and its resets so far [N] i32 (device; either may be NULL). The set
+ * form overrides the shift until the env's next reset (teacher-forced parity). */
+int ps_get_hand_offset(ps_env* env, float* dy, int32_t* episodes, void* stream);
+int ps_set_hand_offset(ps_env* env, const float* dy, void* stream);
 
 #ifdef __cplusplus
 }

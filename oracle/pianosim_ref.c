@@ -26,6 +26,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 #include "../include/pianosim.h"
@@ -136,6 +137,7 @@ typedef struct {
   int h1, b1;        /* side 1: hand/body (kind 2) */
   int h2, b2;        /* side 2: hand/body of the capsule (geom2) */
   int g1, g2;        /* global geom ids (kind 2: both; kind 0/1: g2 only) */
+  int sub;           /* capsule-box: 0/1 = endpoint sphere, 2 = segment point; kind 2: 0 */
   v3 pos, n, t1, t2;
   double dist;
 } contact;
@@ -144,6 +146,8 @@ typedef struct {
   /* state */
   double q[NV], v[NV], qacc_ws[NV], ctrl[PS_NU], sustain, applied[NV];
   int t_idx, last;
+  double hand_dy;  /* randomize_hand_positions: this episode's y shift of both hand roots */
+  int episode;     /* resets so far (the draw counter of hand_dy) */
   /* MidiEvaluationWrapper (wrappers/evaluation.py): sums of the per-step metrics of the
    * running episode, the last finished episode's means, finished-episode count */
   double mus_acc[PS_NMUSIC], mus_ep[PS_NMUSIC];
@@ -159,8 +163,12 @@ typedef struct {
   double M[NH][ND][ND], Mh[NH][ND][ND], D[NH][ND], Dh[NH][ND];
   double Mk[NK], Mkh[NK];
   double bias[NV], passive[NV], actfrc[NV], act_force[PS_NU];
+  /* exact-solve warm start: the previous substep's coupled rows and their free set */
+  int prev_n;
+  uint32_t prev_id[PS_MAX_ROWS];
+  uint8_t prev_free[PS_MAX_ROWS];
   /* collision */
-  int ncon;
+  int ncon, nfound;
   contact con[MAXCON];
   /* outputs */
   double terms[PS_NTERMS];
@@ -175,9 +183,34 @@ struct ref_env {
   float* goal;
   int32_t *count, *keys, *fingers;
   int n;
+  uint64_t seed;
   envdata* e;
 };
 typedef struct ref_env ref_env;
+
+/* Philox4x32-10 (Salmon et al., SC'11), the counter-based generator of the HIP side. */
+static uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+static void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0 = mulhi32(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    uint32_t hi1 = mulhi32(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+/* _randomize_initial_hand_positions (piano_with_shadow_hands.py:491-499):
+ * offset = random_state.uniform(-_POSITION_OFFSET, _POSITION_OFFSET), the same for both hands
+ * (shift_pose (0, offset, 0)). The reference draws from the episode's numpy RandomState; here
+ * the draw is counter-based, keyed by (seed, env, episode), in float: u = 24 random bits /
+ * 2^24, offset = fma(2 * 0.05, u, -0.05). */
+float ref_hand_offset_draw(uint64_t seed, int env, int episode) {
+  uint32_t c[4] = {(uint32_t)episode, (uint32_t)env, 0x68616e64u /* "hand" */, 0u};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float u = (float)(c[0] >> 8) * 0x1p-24f;
+  return fmaf((float)(2.0 * PS_HAND_POSITION_OFFSET), u, (float)-PS_HAND_POSITION_OFFSET);
+}
 
 /* ------------------------------------------------------------------ kinematics */
 static void kinematics(const model* m, envdata* E) {
@@ -190,7 +223,7 @@ static void kinematics(const model* m, envdata* E) {
       v3 pos = mk(d->body_pos[h][b][0], d->body_pos[h][b][1], d->body_pos[h][b][2]);
       m3 R;
       v3 o;
-      if (p < 0) { R = Q; o = pos; }
+      if (p < 0) { R = Q; o = pos; o.v[1] += E->hand_dy; }
       else { R = mm(E->R[h][p], Q); o = add(E->o[h][p], mv(E->R[h][p], pos)); }
       for (int j = m->body_dofadr[h][b]; j >= 0 && j < m->body_dofadr[h][b] + m->body_dofnum[h][b]; j++) {
         v3 al = mk(d->dof_axis[h][j][0], d->dof_axis[h][j][1], d->dof_axis[h][j][2]);
@@ -516,6 +549,7 @@ static double seg_box_t(v3 a, v3 dv, const double* hs) {
 }
 
 static int add_contact(envdata* E, int maxc, const contact* c) {
+  E->nfound++;  /* every contact the narrow phase reports, kept or beyond the cap */
   if (E->ncon >= maxc) return 0;
   E->con[E->ncon++] = *c;
   return 1;
@@ -529,7 +563,7 @@ static void capsule_box(envdata* E, int maxc, contact proto, v3 p0, v3 p1, doubl
     double dist = sphere_box(e == 0 ? p0 : p1, r, c, R, hs, &n, &pos);
     if (dist <= 0.0) {
       contact cc = proto;
-      cc.pos = pos; cc.n = n; cc.dist = dist;
+      cc.pos = pos; cc.n = n; cc.dist = dist; cc.sub = e;
       make_frame(n, &cc.t1, &cc.t2);
       add_contact(E, maxc, &cc);
       found = 1;
@@ -542,7 +576,7 @@ static void capsule_box(envdata* E, int maxc, contact proto, v3 p0, v3 p1, doubl
   double dist = sphere_box(p, r, c, R, hs, &n, &pos);
   if (dist <= 0.0) {
     contact cc = proto;
-    cc.pos = pos; cc.n = n; cc.dist = dist;
+    cc.pos = pos; cc.n = n; cc.dist = dist; cc.sub = 2;
     make_frame(n, &cc.t1, &cc.t2);
     add_contact(E, maxc, &cc);
   }
@@ -574,6 +608,7 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
   const ps_model_desc* d = &m->d;
   int maxc = cfg->max_contacts;
   E->ncon = 0;
+  E->nfound = 0;
   m3 I3 = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
   v3 bc = mk(d->base_pos[0], d->base_pos[1], d->base_pos[2]);
   for (int h = 0; h < NH; h++) {
@@ -622,7 +657,7 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
     cc.dist = dist;
     cc.pos = add(c1, scl(cc.n, ra + 0.5 * dist));
     make_frame(cc.n, &cc.t1, &cc.t2);
-    if (!add_contact(E, maxc, &cc)) break;
+    add_contact(E, maxc, &cc);  /* past the cap: counted in nfound, not kept */
   }
 }
 
@@ -632,7 +667,18 @@ typedef struct {
   double y[NV];   /* L^-T J^T */
   double Aii, R, aref, b, f;
   int closed;     /* free key limit row (solved in closed form) */
+  uint32_t id;    /* identity across substeps (row_id): warm start of the exact solve */
 } row;
+
+/* Row identity: hand limit (dof, side), key limit (key, side), contact edge (capsule, key or
+ * base or capsule, capsule-box sub-contact, pyramid edge). */
+static uint32_t row_id_limit(int dof, int side) { return (0u << 30) | ((uint32_t)dof << 1) | (uint32_t)side; }
+static uint32_t row_id_key(int key, int side) { return (1u << 30) | ((uint32_t)key << 1) | (uint32_t)side; }
+static uint32_t row_id_contact(const contact* c, int edge) {
+  uint32_t cid = c->kind == 2 ? (uint32_t)(NH * NG * (NK + 1) * 3 + c->g1 * NH * NG + c->g2)
+                              : (uint32_t)((c->g2 * (NK + 1) + (c->key < 0 ? NK : c->key)) * 3 + c->sub);
+  return (2u << 30) | (cid << 2) | (uint32_t)edge;
+}
 
 static double impedance(const double* si, double pos) {
   double d0 = clampd(si[0], MINIMP, MAXIMP), dw = clampd(si[1], MINIMP, MAXIMP);
@@ -707,7 +753,151 @@ static _Thread_local row g_rows[MAXROW];
 int ref_debug_level = 0;
 long ref_rows_hist[PS_MAX_ROWS + 2];
 long ref_con_hist[PS_MAX_CONTACTS_LIMIT + 2];
+/* Cap study (per substep): contacts the narrow phase found (kept or not) and coupled rows
+ * requested (before the PS_MAX_ROWS cap), each clamped into the last bin; substeps where a
+ * cap dropped something; sweeps the PGS ran. */
+#define REF_HIST 256
+long ref_found_hist[REF_HIST];
+long ref_rowreq_hist[REF_HIST];
+long ref_cap_events[2];  /* [0] substeps with contacts dropped, [1] with rows dropped */
+long ref_sweeps_total, ref_substeps_total;
+/* Study override of the constraint solve (the specification is cfg->solver, see
+ * dual_solve below):
+ *   0: none (the specification);
+ *   1: PGS run to convergence from a cold start - at least cfg->pgs_iterations sweeps, then
+ *      until a sweep changes no force by more than ref_pgs_tol * (1 + max|f|), at most
+ *      ref_pgs_maxit sweeps. An independent check of the exact solve: the dual is strictly
+ *      convex (R > 0), so both reach the same unique solution. */
+int ref_pgs_mode = 0;
+double ref_pgs_tol = 1e-12;
+int ref_pgs_maxit = 200000;
+long ref_pdas_hist[64];
+FILE* ref_qp_dump;  /* study: append every coupled-row QP here (NULL: off) */  /* linear solves per substep of the exact solve ([63]: iteration cap) */
 #include <stdio.h>
+
+/* Delassus entry of coupled rows i, j: y_i D^-1 y_j (keys: 1 / (I + armature)). */
+static double delassus(const envdata* E, const row* a, const row* b) {
+  double s = 0;
+  for (int k = 0; k < NK; k++) s += a->y[k] * b->y[k] / E->Mk[k];
+  for (int h = 0; h < NH; h++)
+    for (int j = 0; j < ND; j++) s += a->y[NK + h * ND + j] * b->y[NK + h * ND + j] / E->D[h][j];
+  return s;
+}
+
+#define BPP_MAXIT 32
+#define BPP_TOL 1e-10  /* infeasibility below this fraction of max|f| (f) or max|b| (w) is rounding */
+/* Exact solve of the coupled rows' dual problem
+ *     min_f 1/2 f'Hf + b'f   s.t. f >= 0,   H = A + diag(R),  A = J M^-1 J' (Delassus),
+ * the linear complementarity problem w = Hf + b, f >= 0, w >= 0, f'w = 0. Its solution is
+ * unique (H positive definite) and is the constraint force MuJoCo's solvers converge to on
+ * these rows (the default Newton solver minimises the equivalent primal in qacc; pyramidal
+ * cones make every row unilateral).
+ * Method: block principal pivoting (Judice & Pires 1994; Kim & Park's NNLS form): a free set
+ * F gives f_F = -H_FF^-1 b_F (LDL' factorization of H_FF), f = 0 and w = Hf + b elsewhere;
+ * the infeasible rows V = {i in F: f_i < 0} u {i not in F: w_i < 0} are exchanged all at
+ * once while |V| keeps decreasing (3 backup exchanges allowed), otherwise only the largest
+ * index of V (Murty's rule), which terminates for any positive definite H. V empty = the
+ * solution. The start F = {f_i - w_i/H_ii > 0} is the free set of the forces on entry (the
+ * cfg->pgs_iterations warm-up sweeps; with none, {b_i < 0}). Returns the number of solves,
+ * or -1 when BPP_MAXIT solves did not finish (forces = max(0, last iterate)). */
+/* LDL' solve of H_FF x_F = -b_F for the rows fi[0..m) (x = 0 elsewhere) */
+static void solve_free(int n, int m, const int* fi, double H[][MAXROW], const double* bb, double* x) {
+  static _Thread_local double L[MAXROW][MAXROW];
+  double dg[MAXROW], z[MAXROW];
+  for (int a = 0; a < m; a++)
+    for (int c = 0; c <= a; c++) L[a][c] = H[fi[a]][fi[c]];
+  for (int k = 0; k < m; k++) {  /* right-looking LDL' (L unit lower) */
+    dg[k] = L[k][k];
+    for (int a = k + 1; a < m; a++) {
+      double l = L[a][k] / dg[k];
+      for (int c = k + 1; c <= a; c++) L[a][c] -= l * L[c][k];
+    }
+    for (int a = k + 1; a < m; a++) L[a][k] /= dg[k];
+  }
+  for (int a = 0; a < m; a++) {
+    double s = -bb[fi[a]];
+    for (int k = 0; k < a; k++) s -= L[a][k] * z[k];
+    z[a] = s;
+  }
+  for (int a = 0; a < m; a++) z[a] /= dg[a];
+  for (int a = m - 1; a >= 0; a--) {
+    double s = z[a];
+    for (int k = a + 1; k < m; k++) s -= L[k][a] * z[k];
+    z[a] = s;
+  }
+  for (int i = 0; i < n; i++) x[i] = 0.0;
+  for (int a = 0; a < m; a++) x[fi[a]] = z[a];
+}
+
+static int dual_solve(envdata* E, int nr) {
+  int idx[MAXROW], n = 0;
+  for (int i = 0; i < nr; i++)
+    if (!g_rows[i].closed) idx[n++] = i;
+  if (n == 0) { E->prev_n = 0; return 0; }
+  static _Thread_local double H[MAXROW][MAXROW];
+  double bb[MAXROW], f[MAXROW], x[MAXROW], wv[MAXROW];
+  int inF[MAXROW], fi[MAXROW];
+  double bscale = 0.0;
+  for (int i = 0; i < n; i++) {
+    const row* ri = &g_rows[idx[i]];
+    for (int j = 0; j <= i; j++) H[i][j] = H[j][i] = delassus(E, ri, &g_rows[idx[j]]);
+    H[i][i] += ri->R;
+    bb[i] = ri->b;
+    bscale = fmax(bscale, fabs(bb[i]));
+    f[i] = ri->f;  /* after the warm-up sweeps (0 without) */
+  }
+  const double wtol = BPP_TOL * bscale;
+  /* start: a row of the previous substep (same identity) keeps its membership of that
+   * solution's free set; a new row is free if the projected step from the warm-up forces
+   * would make it positive (f_i - w_i / H_ii > 0; with no warm-up: b_i < 0) */
+  for (int i = 0; i < n; i++) {
+    int p = -1;
+    for (int q = 0; q < E->prev_n; q++)
+      if (E->prev_id[q] == g_rows[idx[i]].id) { p = q; break; }
+    if (p >= 0) { inF[i] = E->prev_free[p]; continue; }
+    double s = bb[i];
+    for (int j = 0; j < n; j++) s += H[i][j] * f[j];
+    inF[i] = f[i] - s / H[i][i] > 0.0;
+  }
+  if (ref_qp_dump) {  /* study: n, H (n x n), b, warm-up f, start set */
+    int32_t nn = n;
+    fwrite(&nn, 4, 1, ref_qp_dump);
+    for (int i = 0; i < n; i++) fwrite(H[i], sizeof(double), n, ref_qp_dump);
+    fwrite(bb, sizeof(double), n, ref_qp_dump);
+    fwrite(f, sizeof(double), n, ref_qp_dump);
+    for (int i = 0; i < n; i++) { double v = inF[i]; fwrite(&v, sizeof(double), 1, ref_qp_dump); }
+  }
+  int ninf = n + 1, backup = 3, ret = -1;
+  for (int iter = 1; iter <= BPP_MAXIT; iter++) {
+    int m = 0;
+    for (int i = 0; i < n; i++)
+      if (inF[i]) fi[m++] = i;
+    solve_free(n, m, fi, H, bb, x);
+    double xscale = 0.0;
+    for (int i = 0; i < n; i++) xscale = fmax(xscale, fabs(x[i]));
+    const double ftol = BPP_TOL * xscale;
+    int nv = 0, last = -1;
+    for (int i = 0; i < n; i++) {
+      double s = bb[i];
+      for (int j = 0; j < n; j++) s += H[i][j] * x[j];
+      wv[i] = s;
+      if (inF[i] ? x[i] < -ftol : wv[i] < -wtol) { nv++; last = i; }
+    }
+    if (nv == 0) { ret = iter; break; }
+    if (nv < ninf) { ninf = nv; backup = 3; }
+    else if (backup > 0) backup--;
+    else { inF[last] = !inF[last]; continue; }
+    for (int i = 0; i < n; i++)
+      if (inF[i] ? x[i] < -ftol : wv[i] < -wtol) inF[i] = !inF[i];
+  }
+  E->prev_n = n;
+  for (int i = 0; i < n; i++) {
+    g_rows[idx[i]].f = ret > 0 ? x[i] : fmax(0.0, x[i]);
+    E->prev_id[i] = g_rows[idx[i]].id;
+    E->prev_free[i] = g_rows[idx[i]].f > 0.0;
+  }
+  return ret;
+}
 
 static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
   const ps_model_desc* d = &m->d;
@@ -731,18 +921,21 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
   for (int c = 0; c < E->ncon; c++)
     if (E->con[c].kind == 0) keyhit[E->con[c].key] = 1;
   int nr = 0, ncoup = 0;  /* coupled rows are capped at PS_MAX_ROWS, later ones dropped */
+  int nreq = 4 * E->ncon;  /* coupled rows requested before the cap */
   for (int h = 0; h < NH; h++)
     for (int j = 0; j < ND; j++) {
       if (!d->dof_limited[h][j]) continue;
       double q = E->q[NK + h * ND + j];
       for (int side = 0; side < 2; side++) {
         double dist = side == 0 ? q - d->dof_range[h][j][0] : d->dof_range[h][j][1] - q;
+        if (dist < 0.0) nreq++;
         if (dist >= 0.0 || ncoup >= PS_MAX_ROWS) continue;
         ncoup++;
         row* r = &g_rows[nr++];
         memset(r->J, 0, sizeof(r->J));
         r->J[NK + h * ND + j] = side == 0 ? 1.0 : -1.0;
         r->closed = 0;
+        r->id = row_id_limit(h * ND + j, side);
         row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->dof_invweight[h][j], qacc_smooth);
       }
     }
@@ -753,6 +946,7 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
         double dist = side == 0 ? E->q[k] - d->key_range[k][0] : d->key_range[k][1] - E->q[k];
         if (dist >= 0.0) continue;
         if (pass == 0) {
+          nreq++;
           if (ncoup >= PS_MAX_ROWS) continue;
           ncoup++;
         }
@@ -760,6 +954,7 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
         memset(r->J, 0, sizeof(r->J));
         r->J[k] = side == 0 ? 1.0 : -1.0;
         r->closed = pass;
+        r->id = row_id_key(k, side);
         row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->key_dof_invweight[k], qacc_smooth);
       }
     }
@@ -783,12 +978,17 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       double s = (e & 1) ? -mu : mu;
       for (int i = 0; i < NV; i++) r->J[i] = Jn[i] + s * Jt[i];
       r->closed = 0;
+      r->id = row_id_contact(cc, e);
       row_finish(m, E, r, cc->dist, solref, solimp, diag, qacc_smooth);
     }
   }
 
   __atomic_fetch_add(&ref_rows_hist[ncoup], 1, __ATOMIC_RELAXED); /* ref_step_threads runs envs in parallel */
   __atomic_fetch_add(&ref_con_hist[E->ncon], 1, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&ref_found_hist[E->nfound < REF_HIST ? E->nfound : REF_HIST - 1], 1, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&ref_rowreq_hist[nreq < REF_HIST ? nreq : REF_HIST - 1], 1, __ATOMIC_RELAXED);
+  if (E->nfound > E->ncon) __atomic_fetch_add(&ref_cap_events[0], 1, __ATOMIC_RELAXED);
+  if (nreq > ncoup) __atomic_fetch_add(&ref_cap_events[1], 1, __ATOMIC_RELAXED);
   /* PGS on the coupled rows; closed-form free key rows */
   double w[NV];
   memset(w, 0, sizeof(w));
@@ -801,7 +1001,9 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     r->f = 0.0;
     for (int k = 0; k < NV; k++) w[k] += r->y[k] * r->f;
   }
-  for (int it = 0; it < cfg->pgs_iterations; it++) {
+  int maxit = ref_pgs_mode == 1 ? ref_pgs_maxit : cfg->pgs_iterations, it;
+  for (it = 0; it < maxit; it++) {
+    double dfmax = 0.0, fmaxabs = 0.0;
     for (int i = 0; i < nr; i++) {
       row* r = &g_rows[i];
       if (r->closed) continue;
@@ -815,7 +1017,25 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       if (df != 0.0)
         for (int k = 0; k < NV; k++) w[k] += r->y[k] * df;
       r->f = fn;
+      if (ref_pgs_mode == 1) {  /* (not in the specification's FLOP count) */
+        if (fabs(df) > dfmax) dfmax = fabs(df);
+        if (fabs(fn) > fmaxabs) fmaxabs = fabs(fn);
+      }
     }
+    if (ref_pgs_mode == 1 && it + 1 >= cfg->pgs_iterations && dfmax <= ref_pgs_tol * (1.0 + fmaxabs)) {
+      it++;
+      break;
+    }
+  }
+  __atomic_fetch_add(&ref_sweeps_total, it, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&ref_substeps_total, 1, __ATOMIC_RELAXED);
+  if (ref_pgs_mode == 0 && cfg->solver == PS_SOLVER_EXACT) {
+    int pit = dual_solve(E, nr);
+    __atomic_fetch_add(&ref_pdas_hist[pit >= 0 && pit < 63 ? pit : 63], 1, __ATOMIC_RELAXED);
+    memset(w, 0, sizeof(w));
+    for (int i = 0; i < nr; i++)
+      if (!g_rows[i].closed && g_rows[i].f != 0.0)
+        for (int k = 0; k < NV; k++) w[k] += g_rows[i].y[k] * g_rows[i].f;
   }
   for (int i = 0; i < nr; i++)
     if (g_rows[i].closed)
@@ -930,6 +1150,8 @@ static void key_state(const model* m, envdata* E) {
 }
 
 static void reset_env(ref_env* R, envdata* E, float* obs) {
+  E->hand_dy = R->cfg.randomize_hand_positions ? (double)ref_hand_offset_draw(R->seed, (int)(E - R->e), E->episode) : 0.0;
+  E->episode++;
   memset(E->q, 0, sizeof(E->q));
   memset(E->v, 0, sizeof(E->v));
   memset(E->qacc_ws, 0, sizeof(E->qacc_ws));
@@ -974,6 +1196,7 @@ static void control_step(ref_env* R, envdata* E, const float* a, float* obs, flo
   }
   for (int i = 0; i < PS_NU; i++) E->ctrl[i] = a[i];
   E->sustain = a[PS_NU];
+  E->prev_n = 0;  /* the exact solve's warm start lives within one control step (the GPU's LDS) */
   for (int s = 0; s < d->n_substeps; s++) step_physics(m, &R->cfg, E);
   kinematics(m, E);   /* mj_step1 at the final state (legacy_step) */
   collide(m, &R->cfg, E);
@@ -1108,7 +1331,11 @@ ref_env* ref_create(const ps_model_desc* md, const ps_song_desc* song, const ps_
   memcpy(R->fingers, song->fingers, sizeof(int32_t) * song->T * PS_MAX_NOTES);
   R->n = n;
   R->e = (envdata*)calloc((size_t)n, sizeof(envdata));
-  for (int i = 0; i < n; i++) reset_env(R, &R->e[i], NULL);
+  for (int i = 0; i < n; i++) {
+    reset_env(R, &R->e[i], NULL);
+    R->e[i].episode = 0;  /* as a fresh ps_create: the first ps_reset draws episode 0 */
+    R->e[i].hand_dy = 0.0;
+  }
   return R;
 }
 
@@ -1203,6 +1430,56 @@ void ref_musical_metrics(const ref_env* R, double* episode, int32_t* episodes) {
 
 void ref_contact_count(const ref_env* R, int32_t* ncon) {
   for (int i = 0; i < R->n; i++) ncon[i] = R->e[i].ncon;
+}
+
+void ref_set_seed(ref_env* R, uint64_t seed) { R->seed = seed; }
+void ref_qp_dump_open(const char* path) {
+  if (ref_qp_dump) fclose(ref_qp_dump);
+  ref_qp_dump = path ? fopen(path, "wb") : NULL;
+}
+void ref_get_hand_offset(const ref_env* R, double* dy, int32_t* episode) {
+  for (int i = 0; i < R->n; i++) {
+    if (dy) dy[i] = R->e[i].hand_dy;
+    if (episode) episode[i] = R->e[i].episode;
+  }
+}
+void ref_set_hand_offset(ref_env* R, const double* dy) {
+  for (int i = 0; i < R->n; i++) {
+    envdata* E = &R->e[i];
+    E->hand_dy = dy[i];
+    kinematics(&R->m, E);
+    collide(&R->m, &R->cfg, E);
+    key_state(&R->m, E);
+  }
+}
+
+/* Solver study hooks (see ref_pgs_mode above). */
+void ref_set_solver(int mode, double tol, int maxit) {
+  ref_pgs_mode = mode;
+  ref_pgs_tol = tol;
+  ref_pgs_maxit = maxit;
+}
+void ref_stats_reset(void) {
+  memset(ref_rows_hist, 0, sizeof(ref_rows_hist));
+  memset(ref_con_hist, 0, sizeof(ref_con_hist));
+  memset(ref_found_hist, 0, sizeof(ref_found_hist));
+  memset(ref_rowreq_hist, 0, sizeof(ref_rowreq_hist));
+  memset(ref_cap_events, 0, sizeof(ref_cap_events));
+  ref_sweeps_total = ref_substeps_total = 0;
+  memset(ref_pdas_hist, 0, sizeof(ref_pdas_hist));
+}
+void ref_pdas_hist_get(long* out) { memcpy(out, ref_pdas_hist, sizeof(ref_pdas_hist)); }
+/* found/rowreq [REF_HIST], kept rows [PS_MAX_ROWS + 2], kept contacts [MAXCON + 2],
+ * misc = {substeps with contacts dropped, with rows dropped, sweeps, substeps} */
+void ref_stats_get(long* found, long* rowreq, long* rows, long* cons, long* misc) {
+  memcpy(found, ref_found_hist, sizeof(ref_found_hist));
+  memcpy(rowreq, ref_rowreq_hist, sizeof(ref_rowreq_hist));
+  memcpy(rows, ref_rows_hist, sizeof(ref_rows_hist));
+  memcpy(cons, ref_con_hist, sizeof(ref_con_hist));
+  misc[0] = ref_cap_events[0];
+  misc[1] = ref_cap_events[1];
+  misc[2] = ref_sweeps_total;
+  misc[3] = ref_substeps_total;
 }
 
 /* Single-substep hook for teacher-forced physics parity (no task layer). */

@@ -52,7 +52,47 @@ def _bind(L):
     L.ref_tolerance.argtypes = [C.c_double] * 4
     L.ref_assignment_tol.restype = C.c_double
     L.ref_assignment_tol.argtypes = [C.c_int, C.c_int, _f64p]
+    L.ref_set_solver.argtypes = [C.c_int, C.c_double, C.c_int]
+    L.ref_set_seed.argtypes = [C.c_void_p, C.c_uint64]
+    L.ref_debug_contacts.restype = C.c_int
+    L.ref_debug_contacts.argtypes = [C.c_void_p, C.c_int, _i32p, _f64p]
+    L.ref_get_hand_offset.argtypes = [C.c_void_p, _f64p, _i32p]
+    L.ref_set_hand_offset.argtypes = [C.c_void_p, _f64p]
+    L.ref_hand_offset_draw.restype = C.c_float
+    L.ref_hand_offset_draw.argtypes = [C.c_uint64, C.c_int, C.c_int]
+    _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+    L.ref_stats_get.argtypes = [_i64p] * 5
+    L.ref_pdas_hist_get.argtypes = [_i64p]
     return L
+
+
+STAT_HIST = 256
+
+
+def set_solver(mode: int = 0, tol: float = 1e-12, maxit: int = 200000, counting: bool = False):
+    """Study override: 0 = the specification (cfg.solver); 1 = PGS run to convergence from a
+    cold start (an independent check of the exact solve; pianosim_ref.c ref_pgs_mode)."""
+    (flops_lib() if counting else lib()).ref_set_solver(mode, tol, maxit)
+
+
+def stats_reset():
+    lib().ref_stats_reset()
+
+
+def stats():
+    """Per-substep histograms since stats_reset(): contacts found (before the contact cap),
+    coupled rows requested (before PS_MAX_ROWS), rows kept, contacts kept; and the substeps
+    where a cap dropped contacts / rows, PGS sweeps run, substeps."""
+    found = np.zeros(STAT_HIST, np.int64)
+    rowreq = np.zeros(STAT_HIST, np.int64)
+    rows = np.zeros(64 + 2, np.int64)
+    cons = np.zeros(24 + 2, np.int64)
+    misc = np.zeros(4, np.int64)
+    lib().ref_stats_get(found, rowreq, rows, cons, misc)
+    pdas = np.zeros(64, np.int64)
+    lib().ref_pdas_hist_get(pdas)
+    return dict(found=found, rowreq=rowreq, rows=rows, cons=cons, contact_cap_substeps=int(misc[0]),
+                row_cap_substeps=int(misc[1]), sweeps=int(misc[2]), substeps=int(misc[3]), pdas=pdas)
 
 
 def lib():
@@ -93,8 +133,9 @@ class OracleEnv:
 
     NV, NU, NACTION = 140, 44, 45
 
-    def __init__(self, model_desc, song_tables, cfg, n_envs: int, counting: bool = False):
-        """``counting``: run on the FLOP-counting build (bitwise the same results)."""
+    def __init__(self, model_desc, song_tables, cfg, n_envs: int, counting: bool = False, seed: int = 0):
+        """``counting``: run on the FLOP-counting build (bitwise the same results).
+        ``seed``: key of the randomize_hand_positions draws (as ps_create's)."""
         self._L = flops_lib() if counting else lib()
         from importlib import import_module
         abi = import_module("diffusion-piano_amd.abi")
@@ -112,6 +153,7 @@ class OracleEnv:
         self.n = n_envs
         self._h = self._L.ref_create(C.addressof(model_desc), C.addressof(sd), C.addressof(cfg), n_envs)
         self.obs_dim = self._L.ref_obs_dim(self._h)
+        self._L.ref_set_seed(self._h, seed)
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -184,8 +226,31 @@ class OracleEnv:
         self._L.ref_musical_metrics(self._h, ep, cnt)
         return ep, cnt
 
+    def contacts(self, i):
+        """Contacts of env i after its last step / set_state: [(kind, key, g1, g2, dist)]."""
+        info = np.zeros(4 * 24, np.int32)
+        data = np.zeros(7 * 24)
+        n = self._L.ref_debug_contacts(self._h, i, info, data)
+        return [(int(info[4 * c]), int(info[4 * c + 1]), int(info[4 * c + 2]), int(info[4 * c + 3]), float(data[7 * c]))
+                for c in range(n)]
+
+    def hand_offset(self):
+        """(y shift of both hand roots this episode [N], resets so far [N])."""
+        dy = np.zeros(self.n)
+        ep = np.zeros(self.n, np.int32)
+        self._L.ref_get_hand_offset(self._h, dy, ep)
+        return dy, ep
+
+    def set_hand_offset(self, dy):
+        self._L.ref_set_hand_offset(self._h, np.ascontiguousarray(np.asarray(dy, np.float64).reshape(self.n)))
+
     def physics_substep(self):
         self._L.ref_physics_substep(self._h)
+
+
+def hand_offset_draw(seed: int, env: int, episode: int) -> float:
+    """The randomize_hand_positions draw of (seed, env, episode) (float32, as the GPU's)."""
+    return lib().ref_hand_offset_draw(seed, env, episode)
 
 
 def prf(y_true, y_pred):

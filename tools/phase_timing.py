@@ -11,23 +11,30 @@ from helpers import song
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 L = lib.load()
 L.ps_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
-g = dp.BatchedPianoEnv(N, song(dp, "twinkle"), dp.TaskConfig(), device="cuda:0")
+NAME = sys.argv[2] if len(sys.argv) > 2 else "crossing_field"
+g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle"), device="cuda:0")
 g.reset()
 L.ps_debug_timing(g._h, None)
 gen = torch.Generator(device="cuda:0").manual_seed(1)
+stats = []
 for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
-out = np.zeros((N, 18), np.uint64)
+    stats.append(g.solver_stats().cpu().numpy())
+st = np.stack(stats)  # [10, N, 4]
+out = np.zeros((N, 24), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
 names = {0: "kinematics", 1: "dynamics", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
          3: "factor", 4: "solve_smooth",
          12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T", 15: "cons:finish",
-         16: "pgs:build A", 17: "pgs:sweeps", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
+         16: "pgs:build A", 17: "pgs:sweeps", 18: "ex:rest", 19: "ex:start set", 20: "ex:factor+solve", 21: "ex:w+check", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
 for i, n in names.items():
     v = out[:, i].astype(np.float64)
     print(f"{n:14s} {v.mean()/10:12.0f} cycles/env-step  {100*v.sum()/tot.sum():5.1f}%")
 print(f"total {tot.mean()/10:.0f} cycles/env-step per wave; mean rows/substep {out[:,9].mean()/100:.1f} mean contacts {out[:,10].mean()/100:.2f}")
+solves = st[..., 0] / 10.0
+print(f"exact solve: linear solves per substep mean {solves.mean():.3f}, max over env-steps {st[..., 0].max()} per step; "
+      f"contact-cap substeps {int(st[..., 1].sum())}, row-cap substeps {int(st[..., 2].sum())}, max rows {int(st[..., 3].max())}")
 # the per-env spread sets the tail of a launch (4096 envs = 2 rounds of 2048 slots)
 per = tot / 10
 q = np.percentile(per, [50, 90, 99, 100])
@@ -37,3 +44,10 @@ print(f"per-env cycles/env-step p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max
 for i, n in names.items():
     v = out[top, i].astype(np.float64)
     print(f"  top1% {n:14s} {v.mean()/10:12.0f}")
+# the slowest envs, phase by phase (what sets a launch's tail at one round of workgroups)
+worst = np.argsort(per)[-3:][::-1]
+print("slowest envs (cycles/env-step):", ", ".join(f"{per[w]:.0f}" for w in worst),
+      "| solves per step:", ", ".join(str(int(st[:, w, 0].sum() / 10)) for w in worst),
+      "| max rows:", ", ".join(str(int(st[:, w, 3].max())) for w in worst))
+for i, n in names.items():
+    print(f"  worst {n:14s} " + " ".join(f"{out[w, i] / 10:10.0f}" for w in worst))
