@@ -847,14 +847,9 @@ static int dual_solve(envdata* E, int nr) {
     f[i] = ri->f;  /* after the warm-up sweeps (0 without) */
   }
   const double wtol = BPP_TOL * bscale;
-  /* start: a row of the previous substep (same identity) keeps its membership of that
-   * solution's free set; a new row is free if the projected step from the warm-up forces
-   * would make it positive (f_i - w_i / H_ii > 0; with no warm-up: b_i < 0) */
+  /* start: the free set of the warm-up forces, F = {f_i - w_i / H_ii > 0} (with no warm-up
+   * sweeps: {b_i < 0}) - the HIP kernel's rule */
   for (int i = 0; i < n; i++) {
-    int p = -1;
-    for (int q = 0; q < E->prev_n; q++)
-      if (E->prev_id[q] == g_rows[idx[i]].id) { p = q; break; }
-    if (p >= 0) { inF[i] = E->prev_free[p]; continue; }
     double s = bb[i];
     for (int j = 0; j < n; j++) s += H[i][j] * f[j];
     inF[i] = f[i] - s / H[i][i] > 0.0;
