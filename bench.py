@@ -111,26 +111,43 @@ def cpu_baseline(dp, seq, task, n_envs, steps):
     return out
 
 
-def _profile(name):
+def lib_sha(path=None) -> str:
+    """sha256 (16 hex) of the step kernel's library: profiles record it, and the bench only
+    quotes a profile measured on the very binary it runs."""
+    import hashlib
+
+    p = Path(path) if path else ROOT / "diffusion-piano_amd" / "libpianosim.so"
+    try:
+        return hashlib.sha256(p.read_bytes()).hexdigest()[:16]
+    except OSError:
+        return "missing"
+
+
+def _profile(name, sha=None):
+    """A committed profile; with ``sha``, only if it was measured on that library build."""
     f = ROOT / "profiles" / name
     try:
-        return json.loads(f.read_text()) if f.exists() else None
+        d = json.loads(f.read_text()) if f.exists() else None
     except ValueError:
         return None
+    if d is not None and sha is not None and d.get("lib_sha") != sha:
+        return None
+    return d
 
 
-def pmc_traffic(n_envs, song):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if it matches."""
-    d = _profile("pmc_latest.json")
+def pmc_traffic(n_envs, song, sha):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary of THIS build, else None."""
+    d = _profile("pmc_latest.json", sha)
     if d and d.get("envs") == n_envs and d.get("song", song) == song:
         return d.get("hbm_bytes_per_launch")
     return None
 
 
-def issue_summary(n_envs, song):
+def issue_summary(n_envs, song, sha):
     """Where the wave time goes (the binding limit: latency, not HBM), from the committed SQ
-    counter pass (tools/collect_pmc.py): fractions of the waves' lifetime issuing / waiting."""
-    d = _profile("pmc_latest.json")
+    counter pass of THIS build (tools/collect_pmc.py): fractions of the waves' lifetime
+    issuing / waiting."""
+    d = _profile("pmc_latest.json", sha)
     if d and d.get("envs") == n_envs and d.get("song", song) == song and "wave_issue_frac" in d:
         return {k: d[k] for k in ("wave_issue_frac", "wave_wait_frac", "wave_issue_stall_frac", "valu_insts_per_env_step")}
     return None
@@ -150,13 +167,15 @@ def valu_roofline(song, n_envs, kernel_ms):
             "source": "profiles/flops.json (tools/count_flops.py)"}
 
 
-def drift_summary():
-    """qpos L-inf drift vs the fp64 CPU step, from the committed drift report written by
-    tests/test_gpu_drift.py (PIANOSIM_REPORT=profiles/drift_latest.json)."""
-    d = _profile("drift_latest.json")
+def drift_summary(sha):
+    """qpos L-inf drift vs the fp64 CPU step, from the drift report tests/test_gpu_drift.py
+    wrote for THIS build (PIANOSIM_REPORT=profiles/drift_latest.json; it records the library
+    hash), else None."""
+    d = _profile("drift_latest.json", sha)
     if not d:
         return None
-    out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"), "song": d.get("song")}
+    out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"), "song": d.get("song"),
+           "source": "profiles/drift_latest.json (tests/test_gpu_drift.py, same library build)"}
     chaos = _profile("chaos_floor.json") or {}
     for k in ("zero_action", "trace_actions", "random_actions"):
         if k in d:
@@ -170,18 +189,76 @@ def drift_summary():
     return out
 
 
-def main():
-    args = parse()
+def setup_distributed(backend=None):
+    """One process per GPU (torch.distributed.run env vars). The device is selected BEFORE the
+    process group is created and handed to it (device_id), so RCCL binds this rank's GPU
+    instead of guessing; ``backend`` defaults to nccl (RCCL) with a GPU, gloo without."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dev = torch.device(f"cuda:{local}")
+    else:
+        dev = torch.device("cpu")
+    backend = backend or os.environ.get("PIANOSIM_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return world, rank, local, dev
+
+
+def stagger_episodes(env, global_start, T):
+    """Spread the envs over the episode: env g starts at t_idx = g mod T, so every timed step
+    auto-resets ~N/T envs (reset time included as the episodes roll over)."""
+    t = ((np.arange(env.num_envs) + global_start) % T).astype(np.int32)
+    env.set_state({"t_idx": t})
+
+
+def timed_rollout(env, actions, steps, warmup, dev, returns, sharding):
+    """W untimed steps, then exactly K steps between barrier + device sync on both sides;
+    the wall time is the max over ranks. Also the mean per-step device time of env.step from
+    events on the launch stream (None on CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    dist_on = dist.is_available() and dist.is_initialized()
+    cuda = dev.type == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    pool = len(actions)
+    for i in range(warmup):
+        _, rew, _, st = env.step(actions[i % pool])
+        returns.update(rew, st)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)] if cuda else None
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)] if cuda else None
+    if dist_on:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if cuda:
+            starts[i].record()
+        _, rew, _, st = env.step(actions[(warmup + i) % pool])
+        if cuda:
+            ends[i].record()
+        returns.update(rew, st)
+    sync()
+    if dist_on:
+        dist.barrier()
+    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])) if cuda else None
+    return elapsed, kernel_ms
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local, dev = setup_distributed()
     dp = importlib.import_module("diffusion-piano_amd")
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
     seq, task = load_song(dp, args.song)
@@ -192,35 +269,20 @@ def main():
     pool = max(1, min(args.steps + args.warmup, 64))
     actions = [torch.rand(N, 45, device=dev, generator=gen) * 2 - 1 for _ in range(pool)]
     env.reset()
+    stagger_episodes(env, shard.start, env.song.T)
     returns = sharding.EpisodeReturns(N, dev)
-    for i in range(args.warmup):  # also warms up the (lazily loaded) torch kernels of the return log
-        _, rew, _, st = env.step(actions[i % pool])
-        returns.update(rew, st)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record()
-        _, rew, _, st = env.step(actions[(args.warmup + i) % pool])
-        ends[i].record()
-        returns.update(rew, st)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, device=dev)
+    elapsed, kernel_ms = timed_rollout(env, actions, args.steps, args.warmup, dev, returns, sharding)
     # logging only: RCCL all-gather of the episode returns over xGMI, after the timed region
     fin_sum, fin_n, run_sum, n_all = returns.gather()
     mean_ret = run_sum / n_all
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    stats = env.solver_stats().cpu().numpy()
     total_steps = args.envs * world * args.steps
     value = total_steps / elapsed
     if rank == 0:
+        sha = lib_sha()
         bpe = bytes_per_env_step(env.obs_dim)
         achieved = bpe * N / (kernel_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(N, args.song)
+        traffic = pmc_traffic(N, args.song, sha)
         line = {
             "metric": METRIC,
             "value": value,
@@ -233,18 +295,28 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: uniform random canonical actions (torch Philox, seed 12345+rank)",
+            "data": "synthetic: uniform random canonical actions (torch Philox, seed 12345+rank); episodes "
+                    "staggered (env g starts at t_idx = g mod T) so every step auto-resets ~N/T envs",
             "config": {"workload": f"{N} envs/GPU {args.song} random-action rollout, 10 physics substeps "
-                                   f"per env-step, PGS {task.pgs_iterations} sweeps",
+                                   f"per env-step, exact constraint solve ({task.pgs_iterations} PGS warm-up sweeps "
+                                   f"+ block principal pivoting)",
                        "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
-                       "mean_return_logged": mean_ret, "episodes_finished": fin_n},
+                       "mean_return_logged": mean_ret, "episodes_finished": fin_n,
+                       "lib_sha": sha,
+                       "solver_last_step": {"solves_per_substep": float(stats[:, 0].mean() / 10.0),
+                                            "contact_cap_substeps": int(stats[:, 1].sum()),
+                                            "row_cap_substeps": int(stats[:, 2].sum()),
+                                            "max_rows": int(stats[:, 3].max())}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
-                         "kernel_ms_note": "HIP events around ps_step: order_kernel (counting sort, ~5 us) + pianosim_kernel",
-                         "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song)},
+                         "kernel_ms_note": "HIP events around ps_step on the launch stream: order_kernel "
+                                           "(counting sort, ~5 us) + pianosim_kernel",
+                         "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song, sha),
+                         "profile_note": "traffic / wave_time: rocprofv3 PMC passes of this library build "
+                                         "(profiles/pmc_latest.json lib_sha), null when none exists"},
             "valu_roofline": valu_roofline(args.song, N, kernel_ms),
-            "qpos_drift": drift_summary(),
+            "qpos_drift": drift_summary(sha),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"] = cpu_baseline(dp, seq, task, args.cpu_sample_envs, args.cpu_sample_steps)

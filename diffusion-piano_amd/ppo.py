@@ -594,16 +594,27 @@ class PPOAgent:
         self._fused = None
         self._graph_eager_left = 2
 
-    def _prepare(self, states, actions, rewards, log_probs, next_states, dones):
+    def _prepare(self, states, actions, rewards, log_probs, next_states, dones, valid=None):
         """Reward normalisation, critic values, GAE, advantage normalisation (ppo_v2.py:221-256).
-        Returns (normalised rewards, number of samples)."""
+        ``valid`` (same shape as ``rewards``, optional): samples to train on; the others (an
+        auto-reset's FIRST step: its action had no effect, its "next state" is a new episode)
+        are dropped after GAE, so they enter neither the advantage normalisation nor a
+        minibatch. Returns (normalised rewards, number of samples)."""
         dev = self.device
         s = _f32(states, dev)
         a = _f32(actions, dev)
         lp = _f32(log_probs, dev).reshape(-1)
         ns = _f32(next_states, dev)
         d = _f32(dones, dev)
-        r = self.reward_normalizer(_f32(rewards, dev))
+        raw = _f32(rewards, dev)
+        keep = None
+        if valid is None:
+            r = self.reward_normalizer(raw)
+        else:  # the running statistics see only the samples trained on
+            keep = _f32(valid, dev).reshape(-1) != 0
+            r = torch.zeros_like(raw).reshape(-1)
+            r[keep] = self.reward_normalizer(raw.reshape(-1)[keep]).reshape(-1)
+            r = r.reshape(raw.shape)
         time_major = s.dim() == 3
         with torch.no_grad():
             if time_major:  # [T, E, D]: values of every step, bootstrap from the last next state
@@ -616,21 +627,25 @@ class PPOAgent:
                 values = self.critic(s).squeeze(-1)
                 next_values = self.critic(ns).squeeze(-1)
                 adv, ret = gae(r, values, next_values, d, self.gamma, self.gae_lambda, returns_mode=0)
-        n = adv.numel()
-        adv = normalize_(adv.reshape(-1))
         sdim, adim = s.shape[-1], a.shape[-1]
+        s, a, adv, ret = s.reshape(-1, sdim), a.reshape(-1, adim), adv.reshape(-1), ret.reshape(-1)
+        if keep is not None:
+            s, a, lp, adv, ret = s[keep], a[keep], lp[keep], adv[keep].contiguous(), ret[keep]
+        n = adv.numel()
+        adv = normalize_(adv)
         self._ensure_capacity(n, sdim, adim)
-        self._S[:n].copy_(s.reshape(n, sdim))
-        self._A[:n].copy_(a.reshape(n, adim))
+        self._S[:n].copy_(s)
+        self._A[:n].copy_(a)
         self._LP[:n].copy_(lp)
         self._ADV[:n].copy_(adv)
-        self._RET[:n].copy_(ret.reshape(-1))
+        self._RET[:n].copy_(ret)
         return r, n
 
     # -- update (ppo_v2.py:220-309)
-    def update(self, states, actions, rewards, log_probs, next_states, dones):
+    def update(self, states, actions, rewards, log_probs, next_states, dones, valid=None):
+        """ppo_v2.PPOAgent.update; ``valid`` (optional, this implementation): see _prepare."""
         t0 = time.perf_counter()
-        r, n = self._prepare(states, actions, rewards, log_probs, next_states, dones)
+        r, n = self._prepare(states, actions, rewards, log_probs, next_states, dones, valid)
         B = self.batch_size
         nmb = (n + B - 1) // B
         log = torch.empty(self.ppo_epochs * nmb, len(LOG_KEYS), device=self.device)
@@ -721,6 +736,7 @@ class RolloutTrainer:
         self.logp = torch.empty(H, N, **f32)
         self.rew = torch.empty(H, N, **f32)
         self.done = torch.empty(H, N, **f32)
+        self.valid = torch.empty(H, N, **f32)  # 0 at an auto-reset's FIRST step (action ignored)
         self.ep_return = torch.zeros(N, **f32)
         self.return_sum = torch.zeros((), **f32)  # over finished episodes (device; read when logging)
         self.episodes = torch.zeros((), **f32)
@@ -736,6 +752,7 @@ class RolloutTrainer:
         self.rew[t].copy_(rew)
         done = self.done[t]
         done.copy_(st == abi.LAST)
+        self.valid[t].copy_(st != abi.FIRST)
         self.ep_return += rew
         self.return_sum += (self.ep_return * done).sum()
         self.episodes += done.sum()
@@ -746,11 +763,20 @@ class RolloutTrainer:
         """One outer iteration; returns the number of env-steps taken."""
         N = self.env.num_envs
         if self.reference_semantics:
+            # the reference loop (parallelized_base_v2.py:116-166) steps until all(dones), then
+            # resets: it never updates on a reset transition. Here the envs auto-reset, so a
+            # step whose batch is all FIRST is not trained on, and FIRST rows of a mixed
+            # batch are dropped.
             self._act_step(0)
-            self.agent.update(self.obs[0], self.act[0], self.rew[0], self.logp[0], self._cur, self.done[0])
+            nv = int(self.valid[0].sum().item())
+            if nv == N:
+                self.agent.update(self.obs[0], self.act[0], self.rew[0], self.logp[0], self._cur, self.done[0])
+            elif nv > 0:
+                self.agent.update(self.obs[0], self.act[0], self.rew[0], self.logp[0], self._cur, self.done[0],
+                                  valid=self.valid[0])
             return N
         for t in range(self.horizon):
             self._act_step(t)
         nxt = self._cur.unsqueeze(0)
-        self.agent.update(self.obs, self.act, self.rew, self.logp, nxt, self.done)
+        self.agent.update(self.obs, self.act, self.rew, self.logp, nxt, self.done, valid=self.valid)
         return self.horizon * N

@@ -70,3 +70,72 @@ def test_gloo_world2_gather_and_max():
     res = sorted(q.get(timeout=5) for _ in range(2))
     for rank, s, n, ne, t in res:
         assert s == pytest.approx(sum(range(8))) and n == 8 and ne == 8 and t == 2.0
+
+
+# ------------------------------------------------------------------ bench.py rank logic
+class StubEnv:
+    """bench.py's view of an env on CPU: step() returns (obs, reward, discount, step_type) with
+    an episode of T steps per env (LAST at t_idx == T - 1, FIRST after it), reward 1 per MID."""
+
+    def __init__(self, n, T):
+        self.num_envs, self.T = n, T
+        self.t = torch.zeros(n, dtype=torch.int64)
+        self.last = torch.zeros(n, dtype=torch.bool)
+        self.steps = 0
+
+    def set_state(self, s):
+        self.t = torch.as_tensor(s["t_idx"]).to(torch.int64)
+
+    def step(self, a):
+        self.steps += 1
+        first = self.last.clone()
+        self.t = torch.where(first, torch.zeros_like(self.t), self.t + 1)
+        self.last = ~first & (self.t == self.T)
+        st = torch.where(first, torch.zeros_like(self.t), torch.where(self.last, 2, 1)).to(torch.uint8)
+        rew = torch.where(first, torch.zeros(self.num_envs), torch.ones(self.num_envs))
+        return None, rew, None, st
+
+
+def _bench_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import bench
+    world_, rank_, local, dev = bench.setup_distributed("gloo")
+    try:
+        sh = importlib.import_module("diffusion-piano_amd.sharding")
+        shard = sh.shard_envs(10 * world_, rank_, world_)
+        env = StubEnv(shard.count, T=4)
+        bench.stagger_episodes(env, shard.start, env.T)
+        staggered = env.t.tolist()
+        er = sh.EpisodeReturns(shard.count, dev)
+        elapsed, kms = bench.timed_rollout(env, [None], steps=6, warmup=2, dev=dev, returns=er, sharding=sh)
+        s, n, _, ne = er.gather()
+        q.put((rank_, world_, str(dev), staggered, env.steps, elapsed, kms, n, ne))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_logic_gloo_world2():
+    """bench.py's rank path on CPU: device before the process group, staggered episode phase
+    keyed by global env id, W + K steps, wall time max over ranks, returns gathered."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert [r[0] for r in res] == [0, 1] and all(r[1] == 2 and r[2] == "cpu" for r in res)
+    assert res[0][3] == [g % 4 for g in range(10)] and res[1][3] == [g % 4 for g in range(10, 20)]
+    assert all(r[4] == 8 for r in res)  # warmup + timed steps
+    assert res[0][5] == res[1][5]  # the max over ranks, the same on both
+    assert all(r[6] is None for r in res)  # no device events on CPU
+    # 20 envs, 8 steps from staggered phases of a 4-step episode: episodes end on every rank
+    assert res[0][7] == res[1][7] and res[0][7] > 0 and res[0][8] == 20

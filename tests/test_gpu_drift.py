@@ -85,7 +85,12 @@ def _run(dp, ref, kind):
 
 @pytest.fixture(scope="module")
 def report():
-    rep = {"envs": N, "steps": STEPS, "song": "twinkle", "oracle": "fp64 C restatement (oracle/pianosim_ref.c)"}
+    import sys
+    from helpers import ROOT
+    sys.path.insert(0, str(ROOT))
+    from bench import lib_sha
+    rep = {"envs": N, "steps": STEPS, "song": "twinkle", "oracle": "fp64 C restatement (oracle/pianosim_ref.c)",
+           "lib_sha": lib_sha()}
     yield rep
     path = os.environ.get("PIANOSIM_REPORT")
     if path:

@@ -85,8 +85,9 @@ def test_teacher_forced_step(dp, ref, substep_only):
 
 def test_teacher_forced_many_constraint_rows(dp, ref):
     """States with m hand joints pushed past their limits (m = 4 .. 51), so the coupled
-    constraint rows span every Delassus path: one 16x16 MFMA tile (nrow <= 16), the three
-    tiles of nrow <= 32, and the lane-per-pair build above 32. One physics substep."""
+    constraint rows span every solver path: the register PGS columns (nrow <= 32) and the
+    LDS columns above 32; for the exact solve, the register LDL' templates (free set <= 8,
+    16, 24, 32 rows) and the LDS panel factorization above 32. One physics substep."""
     n = 48
     md, st, tc, g, o = _pair(dp, ref, "twinkle", n, control_timestep=0.005)
     rng = np.random.RandomState(11)

@@ -244,3 +244,43 @@ def test_fused_step_large_minibatch(ppo, tmp_path):
         for (k, p0), (_, p1) in zip(getattr(agents[0], net).named_parameters(), getattr(agents[1], net).named_parameters()):
             g0, g1 = p0.grad.cpu().numpy(), p1.grad.cpu().numpy()
             np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * max(np.abs(g1).max(), 1e-6), err_msg=f"{net}.{k}")
+
+
+def test_rollout_trainer_masks_auto_reset_steps(ppo, tmp_path):
+    """An auto-reset step (FIRST: the kernel ignored the action and reset the env) is not a
+    transition: the horizon rollout marks it invalid and _prepare drops it after GAE (it enters
+    neither the advantage normalisation nor a minibatch); the LAST step before it does not
+    bootstrap (done = 1). The reference-semantics loop skips an all-FIRST step's update, as
+    the reference (which resets after all(dones)) never trains on one."""
+    dp = importlib.import_module("diffusion-piano_amd")
+    N = 16
+    env = dp.BatchedPianoEnv(N, dp.music.test_midi(0.05), dp.TaskConfig(), device="cuda:0")
+    assert env.song.T == 4
+    torch.manual_seed(0)
+    agent = ppo.PPOAgent(env.obs_dim, 45, batch_size=16, ppo_epochs=1, checkpoint_dir=str(tmp_path), use_wandb=False)
+    tr = ppo.RolloutTrainer(env, agent, horizon=8)
+    tr.iterate()
+    valid, done = tr.valid.cpu().numpy(), tr.done.cpu().numpy()
+    assert (valid[4] == 0).all() and valid.sum() == 7 * N  # steps 0-3 episode 1, 4 FIRST, 5-7 episode 2
+    assert (done[3] == 1).all() and done.sum() == N
+    r, n = agent._prepare(tr.obs, tr.act, tr.rew, tr.logp, tr._cur.unsqueeze(0), tr.done, tr.valid)
+    assert n == 7 * N
+    kept = torch.cat([tr.obs[:4], tr.obs[5:]]).reshape(7 * N, -1)
+    assert torch.equal(agent._S[:n], kept)
+    # GAE at the boundary: the LAST step's advantage is its own TD error (no bootstrap)
+    with torch.no_grad():
+        v = agent.critic(tr.obs.reshape(8 * N, -1)).reshape(8, N)
+        nv = agent.critic(tr._cur).reshape(1, N).expand(8, N).contiguous()
+    rn = r.reshape(8, N)
+    adv, ret = ppo.gae(rn, v, nv, tr.done, agent.gamma, agent.gae_lambda, returns_mode=1)
+    torch.testing.assert_close(adv[3], rn[3] - v[3], rtol=1e-5, atol=1e-5)
+    # reference semantics: 4 steps of one episode, then an all-FIRST step with no update
+    calls = []
+    agent2 = ppo.PPOAgent(env.obs_dim, 45, batch_size=16, ppo_epochs=1, checkpoint_dir=str(tmp_path), use_wandb=False)
+    orig = agent2.update
+    agent2.update = lambda *a, **k: (calls.append(k.get("valid") is None), orig(*a, **k))
+    tr2 = ppo.RolloutTrainer(env, agent2, horizon=1, reference_semantics=True)
+    for _ in range(5):
+        tr2.iterate()
+    assert calls == [True] * 4
+    env.close()

@@ -48,7 +48,9 @@ def main():
     stats = [r for r in rows(tdir, "*kernel_stats.csv") if "pianosim_kernel" in r.get("Name", "")]
     fetch_kb = counter(fdir, "FETCH_SIZE")
     write_kb = counter(wdir, "WRITE_SIZE")
-    out = {"envs": envs, "song": song, "kernel": "pianosim_kernel"}
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench import lib_sha  # the profiled binary (bench.py quotes only profiles of its own build)
+    out = {"envs": envs, "song": song, "kernel": "pianosim_kernel", "lib_sha": lib_sha()}
     if stats:
         s = stats[0]
         out["rocprof_avg_ns_all_launches"] = float(s.get("AverageNs", 0))

@@ -56,10 +56,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local)  # the device first, then the process group bound to it
     dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group(os.environ.get("PIANOSIM_DIST_BACKEND", "nccl"), device_id=dev)
     dp = importlib.import_module("diffusion-piano_amd")
     ppo = importlib.import_module("diffusion-piano_amd.ppo")
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
