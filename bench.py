@@ -298,7 +298,7 @@ def main():
             "data": "synthetic: uniform random canonical actions (torch Philox, seed 12345+rank); episodes "
                     "staggered (env g starts at t_idx = g mod T) so every step auto-resets ~N/T envs",
             "config": {"workload": f"{N} envs/GPU {args.song} random-action rollout, 10 physics substeps "
-                                   f"per env-step, exact constraint solve ({task.pgs_iterations} PGS warm-up sweeps "
+                                   f"per env-step, exact constraint solve ({env.task_cfg.pgs_iterations} PGS warm-up sweeps "
                                    f"+ block principal pivoting)",
                        "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
                        "mean_return_logged": mean_ret, "episodes_finished": fin_n,

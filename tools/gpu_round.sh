@@ -23,8 +23,8 @@ timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 cp gpurun_out/bench.json profiles/${P}_bench.json
 # per-phase cycle split from the -DPS_TIMING build (built on the CPU side beforehand)
 if [ -f diffusion-piano_amd/libpianosim_timing.so ]; then
-  (echo "# tools/phase_timing.py 4096 (PIANOSIM_LIB=libpianosim_timing.so, -DPS_TIMING), MI355X, Twinkle random actions";
-   PIANOSIM_LIB=diffusion-piano_amd/libpianosim_timing.so timeout -k 10 120 python tools/phase_timing.py 4096) > profiles/${P}_phase_timing.txt 2>/dev/null || exit 5
+  (echo "# tools/phase_timing.py 4096 crossing_field (PIANOSIM_LIB=libpianosim_timing.so, -DPS_TIMING), MI355X, random actions";
+   PIANOSIM_LIB=diffusion-piano_amd/libpianosim_timing.so timeout -k 10 120 python tools/phase_timing.py 4096 crossing_field) > profiles/${P}_phase_timing.txt 2>/dev/null || exit 5
 fi
 timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 > profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/throughput.py twinkle 1024 4096 >> profiles/${P}_throughput.txt 2>/dev/null || exit 6
