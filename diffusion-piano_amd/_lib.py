@@ -16,7 +16,7 @@ EXPORTS = (
     "ps_last_error", "ps_version", "ps_obs_dim", "ps_model_desc_size", "ps_create", "ps_destroy",
     "ps_reset", "ps_step", "ps_get_state", "ps_set_state", "ps_set_applied", "ps_reward_terms",
     "ps_fingertips", "ps_contact_count", "ps_musical_metrics", "ps_solver_stats", "ps_get_hand_offset",
-    "ps_set_hand_offset",
+    "ps_set_hand_offset", "ps_record_contacts", "ps_contacts",
 )
 
 # Every entry point declared in include/pianorl.h.
@@ -56,7 +56,10 @@ def load() -> C.CDLL:
     L.ps_fingertips.argtypes = [vp, vp, vp]
     L.ps_contact_count.argtypes = [vp, vp, vp]
     L.ps_musical_metrics.argtypes = [vp, vp, vp, vp]
-    for name, argc in (("ps_solver_stats", 3), ("ps_get_hand_offset", 4), ("ps_set_hand_offset", 3)):
+    if hasattr(L, "ps_record_contacts"):
+        L.ps_record_contacts.argtypes = [vp, i32]
+    for name, argc in (("ps_solver_stats", 3), ("ps_get_hand_offset", 4), ("ps_set_hand_offset", 3),
+                       ("ps_contacts", 3)):
         if hasattr(L, name):  # (absent from older builds loaded for A/B runs via PIANOSIM_LIB)
             getattr(L, name).argtypes = [vp] * argc
     for name in EXPORTS:

@@ -14,6 +14,11 @@ NV = NKEY + NHAND * HAND_NDOF
 NU = NHAND * HAND_NACT
 NACTION = NU + 1
 MAX_CAPPAIRS = 768
+HAND_NXGEOM = 12       # box / convex-hull colliders per hand
+HULL_MAXVERT = 64
+HAND_HULLVERT = 384
+MAX_XPAIRS = 1024
+GEOM_NONE, GEOM_BOX, GEOM_HULL = 0, 1, 2
 MAX_NOTES = 16
 MAX_CONTACTS_LIMIT = 24
 MAX_ROWS = 64
@@ -69,6 +74,11 @@ class ModelDesc(C.Structure):
         ("n_cappairs", i32), ("cappair", _arr(i32, MAX_CAPPAIRS, 2)),
         ("key_body_invweight", _arr(d, NKEY)), ("key_dof_invweight", _arr(d, NKEY)),
         ("body_invweight", _arr(d, NHAND, HAND_NBODY)), ("dof_invweight", _arr(d, NHAND, HAND_NDOF)),
+        ("xgeom_type", _arr(i32, NHAND, HAND_NXGEOM)), ("xgeom_body", _arr(i32, NHAND, HAND_NXGEOM)),
+        ("xgeom_pos", _arr(d, NHAND, HAND_NXGEOM, 3)), ("xgeom_quat", _arr(d, NHAND, HAND_NXGEOM, 4)),
+        ("xgeom_size", _arr(d, NHAND, HAND_NXGEOM, 3)), ("xgeom_rbound", _arr(d, NHAND, HAND_NXGEOM)),
+        ("xgeom_vert", _arr(i32, NHAND, HAND_NXGEOM, 2)), ("hull_vert", _arr(d, NHAND, HAND_HULLVERT, 3)),
+        ("n_xpairs", i32), ("xpair", _arr(i32, MAX_XPAIRS, 2)),
     ]
 
 

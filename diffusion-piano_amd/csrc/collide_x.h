@@ -1,0 +1,444 @@
+// collide_x.h - narrow phases of the box and convex-hull hand colliders (MuJoCo geom types
+// box and mesh; the Menagerie hand's palm boxes and distal meshes, shadow_hand.py:95,144-152):
+// Minkowski portal refinement for every pair with a hull (libccd's ccdMPRPenetration, what
+// MuJoCo's mjc_Convex runs for meshes: one contact), separating axes + face clipping for
+// box-box (up to 4 contacts), and capsule vs oriented box. Stated sequentially in
+// oracle/pianosim_ref.c (support, mpr_penetration, box_box, extra_pair); this is the same
+// algorithm in fp32, one pair per lane, registers only (no scratch: every small array is
+// indexed by unrolled loops).
+#pragma once
+#include "prims.h"
+
+namespace ps {
+
+// world collider of a lane's narrow phase
+struct XShape {
+  int type;        // 0 capsule, PS_GEOM_BOX, PS_GEOM_HULL
+  f3 c;            // centre (capsule: segment midpoint)
+  float R[9];      // rotation (box / hull), row-major
+  f3 p0, p1;       // capsule segment
+  float r;         // capsule radius
+  f3 hs;           // box half sizes
+  int v0, nv;      // hull vertices in DevModel::hull_v (geom frame)
+};
+
+__device__ __forceinline__ void quat_to_R(float w, float x, float y, float z, float* R) {
+  const float n = rsqrtf(w * w + x * x + y * y + z * z);
+  w *= n; x *= n; y *= n; z *= n;
+  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - w * z); R[2] = 2.f * (x * z + w * y);
+  R[3] = 2.f * (x * y + w * z); R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - w * x);
+  R[6] = 2.f * (x * z - w * y); R[7] = 2.f * (y * z + w * x); R[8] = 1.f - 2.f * (x * x + y * y);
+}
+// rotation matrix -> unit quaternion (Shepperd's method)
+__device__ __forceinline__ void R_to_quat(const float* R, float* q) {
+  const float t = R[0] + R[4] + R[8];
+  if (t > 0.f) {
+    const float s = sqrtf(t + 1.f) * 2.f, i = 1.f / s;
+    q[0] = 0.25f * s; q[1] = (R[7] - R[5]) * i; q[2] = (R[2] - R[6]) * i; q[3] = (R[3] - R[1]) * i;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    const float s = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f, i = 1.f / s;
+    q[0] = (R[7] - R[5]) * i; q[1] = 0.25f * s; q[2] = (R[1] + R[3]) * i; q[3] = (R[2] + R[6]) * i;
+  } else if (R[4] > R[8]) {
+    const float s = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f, i = 1.f / s;
+    q[0] = (R[2] - R[6]) * i; q[1] = (R[1] + R[3]) * i; q[2] = 0.25f * s; q[3] = (R[5] + R[7]) * i;
+  } else {
+    const float s = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f, i = 1.f / s;
+    q[0] = (R[3] - R[1]) * i; q[1] = (R[2] + R[6]) * i; q[2] = (R[5] + R[7]) * i; q[3] = 0.25f * s;
+  }
+}
+
+__device__ __forceinline__ float sgn0f(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+__device__ __forceinline__ f3 nrmz3(f3 a) {
+  const float n = norm3(a);
+  return n > 0.f ? a * (1.f / n) : a;
+}
+
+// support point in direction d (the CPU checker's support(): box corner by sign, 0 on a zero
+// component; capsule end by sign along the axis + radius along d; hull: first maximal vertex)
+__device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XShape& s, f3 d) {
+  if (s.type == 0) {
+    const f3 ax = s.p1 - s.p0;
+    const float da = dot3(ax, d), dn = norm3(d);
+    const f3 base = da > 0.f ? s.p1 : (da < 0.f ? s.p0 : (s.p0 + s.p1) * 0.5f);
+    return dn > 0.f ? base + d * (s.r / dn) : base;
+  }
+  const f3 dl = mtv3(s.R, d);
+  f3 loc;
+  if (s.type == PS_GEOM_BOX) {
+    loc = mk3(sgn0f(dl.x) * s.hs.x, sgn0f(dl.y) * s.hs.y, sgn0f(dl.z) * s.hs.z);
+  } else {
+    float bd = -INFINITY;
+    loc = mk3(0.f, 0.f, 0.f);
+    for (int i = 0; i < s.nv; i++) {
+      const float4 v = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + i]);
+      const float p = dl.x * v.x + dl.y * v.y + dl.z * v.z;
+      if (p > bd) { bd = p; loc = mk3(v.x, v.y, v.z); }
+    }
+  }
+  return s.c + mv3(s.R, loc);
+}
+
+// ------------------------------------------------------------------ MPR
+constexpr float MPR_TOLF = 1e-6f;
+constexpr int MPR_MAXITF = 50;
+constexpr float MPR_EPSF = 2.220446049250313e-16f;  // the double build's CCD_EPS (MuJoCo's libccd), as the checker
+struct MprPt {
+  f3 v, a, b;
+};
+__device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < MPR_EPSF; }
+__device__ __forceinline__ MprPt mpr_sup(const DevModel* __restrict__ m, const XShape& A, const XShape& B, f3 d) {
+  MprPt p;
+  p.a = x_support(m, A, d);
+  p.b = x_support(m, B, d * -1.f);
+  p.v = p.a - p.b;
+  return p;
+}
+__device__ __forceinline__ f3 portal_dir(const MprPt& p1, const MprPt& p2, const MprPt& p3) {
+  return nrmz3(cross3(p2.v - p1.v, p3.v - p1.v));
+}
+__device__ __forceinline__ bool portal_reach_tol(const MprPt& p1, const MprPt& p2, const MprPt& p3, const MprPt& v4, f3 dir) {
+  const float d4 = dot3(v4.v, dir);
+  const float mn = fminf(d4 - dot3(p1.v, dir), fminf(d4 - dot3(p2.v, dir), d4 - dot3(p3.v, dir)));
+  return mn <= MPR_TOLF;
+}
+__device__ __forceinline__ void expand_portal(const MprPt& p0, MprPt& p1, MprPt& p2, MprPt& p3, const MprPt& v4) {
+  const f3 v4v0 = cross3(v4.v, p0.v);
+  if (dot3(p1.v, v4v0) > 0.f) {
+    if (dot3(p2.v, v4v0) > 0.f) p1 = v4; else p3 = v4;
+  } else {
+    if (dot3(p3.v, v4v0) > 0.f) p2 = v4; else p1 = v4;
+  }
+}
+// closest point of triangle (a, b, c) to the origin (Ericson, RTCD 5.1.5)
+__device__ __forceinline__ f3 tri_closest_origin(f3 a, f3 b, f3 c) {
+  const f3 ab = b - a, ac = c - a, ap = a * -1.f;
+  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) return a;
+  const f3 bp = b * -1.f;
+  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) return b;
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + ab * (d1 / (d1 - d3));
+  const f3 cp = c * -1.f;
+  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0.f && d5 <= d6) return c;
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + ac * (d2 / (d2 - d6));
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + (c - b) * ((d4 - d3) / ((d4 - d3) + (d5 - d6)));
+  const float den = 1.f / (va + vb + vc);
+  return a + ab * (vb * den) + ac * (vc * den);
+}
+__device__ __forceinline__ f3 mpr_pos(const MprPt& p0, const MprPt& p1, const MprPt& p2, const MprPt& p3) {
+  const f3 dir = portal_dir(p1, p2, p3);
+  float b0 = dot3(cross3(p1.v, p2.v), p3.v), b1 = dot3(cross3(p3.v, p2.v), p0.v);
+  float b2 = dot3(cross3(p0.v, p1.v), p3.v), b3 = dot3(cross3(p2.v, p1.v), p0.v);
+  float sum = b0 + b1 + b2 + b3;
+  if (mpr_zero(sum) || sum < 0.f) {
+    b0 = 0.f;
+    b1 = dot3(cross3(p2.v, p3.v), dir);
+    b2 = dot3(cross3(p3.v, p1.v), dir);
+    b3 = dot3(cross3(p1.v, p2.v), dir);
+    sum = b1 + b2 + b3;
+  }
+  const float inv = 1.f / sum;
+  const f3 pa = p0.a * b0 + p1.a * b1 + p2.a * b2 + p3.a * b3;
+  const f3 pb = p0.b * b0 + p1.b * b1 + p2.b * b2 + p3.b * b3;
+  return (pa * inv + pb * inv) * 0.5f;
+}
+// 1: penetrating (depth >= 0, normal A -> B, contact point); 0: apart
+__device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
+                                               float* depth, f3* n, f3* pos) {
+  MprPt p0, p1, p2, p3;
+  p0.a = A.c; p0.b = B.c; p0.v = A.c - B.c;
+  if (p0.v.x == 0.f && p0.v.y == 0.f && p0.v.z == 0.f) p0.v.x += 10.f * MPR_EPSF;
+  f3 dir = nrmz3(p0.v * -1.f);
+  p1 = mpr_sup(m, A, B, dir);
+  float dt = dot3(p1.v, dir);
+  if (mpr_zero(dt) || dt < 0.f) return 0;
+  dir = cross3(p0.v, p1.v);
+  if (mpr_zero(dot3(dir, dir))) {
+    *pos = (p1.a + p1.b) * 0.5f;
+    if (p1.v.x == 0.f && p1.v.y == 0.f && p1.v.z == 0.f) { *depth = 0.f; *n = mk3(0.f, 0.f, 0.f); }
+    else { *depth = norm3(p1.v); *n = nrmz3(p1.v); }
+    return 1;
+  }
+  dir = nrmz3(dir);
+  p2 = mpr_sup(m, A, B, dir);
+  dt = dot3(p2.v, dir);
+  if (mpr_zero(dt) || dt < 0.f) return 0;
+  dir = nrmz3(cross3(p1.v - p0.v, p2.v - p0.v));
+  if (dot3(dir, p0.v) > 0.f) { const MprPt t = p1; p1 = p2; p2 = t; dir = dir * -1.f; }
+  for (int it = 0;; it++) {
+    if (it > 4 * MPR_MAXITF) return 0;
+    p3 = mpr_sup(m, A, B, dir);
+    dt = dot3(p3.v, dir);
+    if (mpr_zero(dt) || dt < 0.f) return 0;
+    bool cont = false;
+    float t = dot3(cross3(p1.v, p3.v), p0.v);
+    if (t < 0.f && !mpr_zero(t)) { p2 = p3; cont = true; }
+    if (!cont) {
+      t = dot3(cross3(p3.v, p2.v), p0.v);
+      if (t < 0.f && !mpr_zero(t)) { p1 = p3; cont = true; }
+    }
+    if (!cont) break;
+    dir = nrmz3(cross3(p1.v - p0.v, p2.v - p0.v));
+  }
+  for (int it = 0;; it++) {
+    if (it > 4 * MPR_MAXITF) return 0;
+    dir = portal_dir(p1, p2, p3);
+    dt = dot3(p1.v, dir);
+    if (mpr_zero(dt) || dt > 0.f) break;
+    const MprPt v4 = mpr_sup(m, A, B, dir);
+    const float d4 = dot3(v4.v, dir);
+    if (!(mpr_zero(d4) || d4 > 0.f) || portal_reach_tol(p1, p2, p3, v4, dir)) return 0;
+    expand_portal(p0, p1, p2, p3, v4);
+  }
+  for (int it = 0;; it++) {
+    dir = portal_dir(p1, p2, p3);
+    const MprPt v4 = mpr_sup(m, A, B, dir);
+    if (portal_reach_tol(p1, p2, p3, v4, dir) || it > MPR_MAXITF) {
+      const f3 cp = tri_closest_origin(p1.v, p2.v, p3.v);
+      *depth = norm3(cp);
+      *n = mpr_zero(*depth) ? dir : cp * (1.f / *depth);
+      *pos = mpr_pos(p0, p1, p2, p3);
+      return 1;
+    }
+    expand_portal(p0, p1, p2, p3, v4);
+  }
+}
+
+// ------------------------------------------------------------------ box-box
+// Small fixed arrays indexed by a run-time count: written through unrolled selects so they
+// stay in registers.
+template <int N>
+__device__ __forceinline__ void put3(f3 (&a)[N], int i, f3 v) {
+#pragma unroll
+  for (int j = 0; j < N; j++)
+    if (j == i) a[j] = v;
+}
+template <int N>
+__device__ __forceinline__ f3 get3(const f3 (&a)[N], int i) {
+  f3 r = a[0];
+#pragma unroll
+  for (int j = 1; j < N; j++)
+    if (j == i) r = a[j];
+  return r;
+}
+__device__ __forceinline__ f3 rcol(const float* R, int i) { return mk3(R[i], R[3 + i], R[6 + i]); }
+__device__ __forceinline__ float f3c(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+constexpr int BB_MAXPT = 4;
+// separating axes + reference-face clipping (the CPU checker's box_box, same rules and order)
+__device__ __forceinline__ int box_box(const XShape& A, const XShape& B, f3 (&pos)[BB_MAXPT], float (&dist)[BB_MAXPT],
+                                       f3* nout) {
+  f3 a[3], b[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) { a[i] = rcol(A.R, i); b[i] = rcol(B.R, i); }
+  const f3 t = B.c - A.c;
+  float best = INFINITY;
+  int bax = -1;
+  f3 bn = mk3(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    f3 L;
+    if (k < 3) L = a[k];
+    else if (k < 6) L = b[k - 3];
+    else {
+      L = cross3(a[(k - 6) / 3], b[(k - 6) % 3]);
+      const float ln = norm3(L);
+      if (ln < 1e-6f) continue;
+      L = L * (1.f / ln);
+    }
+    float ra = 0.f, rb = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      ra += f3c(A.hs, i) * fabsf(dot3(a[i], L));
+      rb += f3c(B.hs, i) * fabsf(dot3(b[i], L));
+    }
+    const float s = dot3(t, L);
+    const float ov = ra + rb - fabsf(s);
+    if (ov < 0.f) return 0;
+    if (k < 6 ? ov < best : 1.05f * ov < best) { best = ov; bax = k; bn = s >= 0.f ? L : L * -1.f; }
+  }
+  if (bax >= 6) {  // edge-edge
+    const int i = (bax - 6) / 3, j = (bax - 6) % 3;
+    f3 pa = A.c, pb = B.c, ai = a[0], bj = b[0];
+    float hai = A.hs.x, hbj = B.hs.x;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (k != i) pa = pa + a[k] * ((dot3(a[k], bn) >= 0.f ? 1.f : -1.f) * f3c(A.hs, k));
+      else { ai = a[k]; hai = f3c(A.hs, k); }
+      if (k != j) pb = pb + b[k] * ((dot3(b[k], bn) >= 0.f ? -1.f : 1.f) * f3c(B.hs, k));
+      else { bj = b[k]; hbj = f3c(B.hs, k); }
+    }
+    f3 c1, c2;
+    seg_seg(pa - ai * hai, pa + ai * hai, pb - bj * hbj, pb + bj * hbj, &c1, &c2);
+    pos[0] = (c1 + c2) * 0.5f;
+    dist[0] = -best;
+    *nout = bn;
+    return 1;
+  }
+  const bool refA = bax < 3;
+  const int fi = refA ? bax : bax - 3;
+  const XShape& Rf = refA ? A : B;
+  const XShape& In = refA ? B : A;
+  f3 ra[3], ia[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { ra[k] = refA ? a[k] : b[k]; ia[k] = refA ? b[k] : a[k]; }
+  const f3 nf = refA ? bn : bn * -1.f;
+  int ij = 0;
+  float bd = -1.f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float d = fabsf(dot3(ia[k], nf));
+    if (d > bd) { bd = d; ij = k; }
+  }
+  const f3 iaj = ij == 0 ? ia[0] : (ij == 1 ? ia[1] : ia[2]);
+  const float sg = dot3(iaj, nf) > 0.f ? -1.f : 1.f;
+  const int u = (ij + 1) % 3, w = (ij + 2) % 3;
+  const f3 iau = u == 0 ? ia[0] : (u == 1 ? ia[1] : ia[2]);
+  const f3 iaw = w == 0 ? ia[0] : (w == 1 ? ia[1] : ia[2]);
+  const float hu = f3c(In.hs, u), hw = f3c(In.hs, w);
+  const f3 fc = In.c + iaj * (sg * f3c(In.hs, ij));
+  f3 poly[8];
+  poly[0] = fc + iau * hu + iaw * hw;
+  poly[1] = fc - iau * hu + iaw * hw;
+  poly[2] = fc - iau * hu - iaw * hw;
+  poly[3] = fc + iau * hu - iaw * hw;
+#pragma unroll
+  for (int k = 4; k < 8; k++) poly[k] = poly[0];
+  int np = 4;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int ax = (fi + 1 + e / 2) % 3;
+    const f3 rax = ax == 0 ? ra[0] : (ax == 1 ? ra[1] : ra[2]);
+    const f3 pn = (e % 2) ? rax * -1.f : rax;
+    const float off = dot3(pn, Rf.c) + f3c(Rf.hs, ax);
+    f3 tmp[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) tmp[k] = poly[0];
+    int nq = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (k < np) {
+        const f3 p = poly[k], q = k + 1 < 8 ? (k + 1 < np ? poly[(k + 1) & 7] : poly[0]) : poly[0];
+        const float dp = dot3(pn, p) - off, dq = dot3(pn, q) - off;
+        if (dp <= 0.f) { put3(tmp, nq, p); nq++; }
+        if ((dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f)) { put3(tmp, nq, p + (q - p) * (dp / (dp - dq))); nq++; }
+      }
+    }
+    np = nq;
+#pragma unroll
+    for (int k = 0; k < 8; k++) poly[k] = tmp[k];
+    if (np == 0) return 0;
+  }
+  const float fo = dot3(nf, Rf.c) + f3c(Rf.hs, fi);
+  f3 cp[8];
+  float cd[8];
+  int nc = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) cp[k] = poly[0];
+#pragma unroll
+  for (int k = 0; k < 8; k++) cd[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k < np) {
+      const float d = fo - dot3(nf, poly[k]);
+      if (d >= 0.f) {
+        put3(cp, nc, poly[k]);
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (j == nc) cd[j] = d;
+        nc++;
+      }
+    }
+  }
+  // deepest first, then farthest-point sampling (ties: lowest index)
+  int ns = 0;
+  uint32_t used = 0;
+  float md[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) md[k] = INFINITY;
+  for (int q = 0; q < BB_MAXPT; q++) {
+    if (q >= nc) break;
+    int bi = -1;
+    float bv = -1.f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (k < nc && !((used >> k) & 1u)) {
+        const float v = q == 0 ? cd[k] : md[k];
+        if (v > bv) { bv = v; bi = k; }
+      }
+    }
+    used |= 1u << bi;
+    const f3 pq = get3(cp, bi);
+    float dq = cd[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++)
+      if (k == bi) dq = cd[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) md[k] = fminf(md[k], norm3(cp[k] - pq));
+#pragma unroll
+    for (int j = 0; j < BB_MAXPT; j++)
+      if (j == q) { pos[j] = pq + nf * (0.5f * dq); dist[j] = -dq; }
+    ns++;
+  }
+  *nout = bn;
+  return ns;
+}
+
+// capsule vs oriented box (box = geom1, normal box -> capsule; the checker's capsule_box with
+// a general box frame): endpoint spheres, else the segment point closest to the box
+__device__ __forceinline__ int capsule_obox(const XShape& C, const XShape& Bx, f3 (&pos)[BB_MAXPT], float (&dist)[BB_MAXPT],
+                                            f3 (&nrm)[BB_MAXPT]) {
+  const float hs[3] = {Bx.hs.x, Bx.hs.y, Bx.hs.z};
+  int n = 0;
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    f3 nn, pp;
+    const float d = sphere_box(e == 0 ? C.p0 : C.p1, C.r, Bx.c, Bx.R, hs, &nn, &pp);
+    if (d <= 0.f) {
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+        if (j == n) { pos[j] = pp; dist[j] = d; nrm[j] = nn; }
+      n++;
+    }
+  }
+  if (n) return n;
+  const f3 la = mtv3(Bx.R, C.p0 - Bx.c), lb = mtv3(Bx.R, C.p1 - Bx.c);
+  const float t = seg_box_t(la, lb - la, hs);
+  f3 nn, pp;
+  const float d = sphere_box(C.p0 + (C.p1 - C.p0) * t, C.r, Bx.c, Bx.R, hs, &nn, &pp);
+  if (d <= 0.f) { pos[0] = pp; dist[0] = d; nrm[0] = nn; return 1; }
+  return 0;
+}
+
+// Narrow phase of collider A (geom1) with collider B: capsule-box (the box becomes geom1:
+// swap = true, normal box -> capsule), box-box, or MPR for every pair with a hull. Returns the
+// contact count (<= 4); normals point geom1 -> geom2.
+__device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
+                                        f3 (&pos)[BB_MAXPT], float (&dist)[BB_MAXPT], f3 (&nrm)[BB_MAXPT], bool& swap) {
+  swap = false;
+  if (A.type == 0 && B.type == PS_GEOM_BOX) {
+    swap = true;
+    return capsule_obox(A, B, pos, dist, nrm);
+  }
+  if (A.type == PS_GEOM_BOX && B.type == PS_GEOM_BOX) {
+    f3 n;
+    const int cnt = box_box(A, B, pos, dist, &n);
+#pragma unroll
+    for (int j = 0; j < BB_MAXPT; j++) nrm[j] = n;
+    return cnt;
+  }
+  float depth;
+  f3 n, p;
+  const int cnt = mpr_penetration(m, A, B, &depth, &n, &p);
+  if (n.x == 0.f && n.y == 0.f && n.z == 0.f) n = mk3(0.f, 0.f, 1.f);
+  pos[0] = p;
+  nrm[0] = n;
+  dist[0] = -depth;
+  return cnt;
+}
+
+}  // namespace ps

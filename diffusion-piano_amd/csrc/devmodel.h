@@ -19,6 +19,10 @@ constexpr int NU = PS_NU;
 constexpr int NBT = NH * NB;   // 50 hand bodies
 constexpr int NDT = NH * ND;   // 52 hand dofs (lane l <-> hand dof l)
 constexpr int NGT = NH * NG;   // 40 capsules
+constexpr int NX = PS_HAND_NXGEOM;
+constexpr int NXT = NH * NX;   // 24 box / hull colliders: lanes NGT .. NGT + NXT - 1
+constexpr int NCOLL = NGT + NXT;  // global collider ids: capsules, then the extra colliders
+static_assert(NCOLL <= 64, "one lane per collider");
 constexpr int NTT = NH * PS_HAND_NTENDON;
 constexpr int MAXDEP = 9;      // ancestor list length (self + up to 8 ancestors)
 constexpr int MAXLEV = 8;      // body tree levels
@@ -68,8 +72,8 @@ struct DevModel {
   // actuators, global a = h*NA + a
   int act_kind[NU], act_dof0[NU], act_dof1[NU], act_flim[NU];
   float act_c0[NU], act_c1[NU], act_kp[NU], act_clo[NU], act_chi[NU], act_flo[NU], act_fhi[NU];
-  // capsules
-  int geom_body[NGT];
+  // colliders: the body of every collider (capsules, then extras); capsule geometry
+  int geom_body[NCOLL];
   float geom_pos[NGT][3], geom_axis[NGT][3], geom_hl[NGT], geom_r[NGT];
   int root_geom_count;
   // fingertip sites
@@ -78,6 +82,14 @@ struct DevModel {
   // capsule-capsule pairs
   int npairs;
   int pair[PS_MAX_CAPPAIRS][2];
+  // extra (box / hull) colliders, global extra index e = h*NX + i (lane NGT + e)
+  int nx;                      // extra colliders in use (0: the extra passes are skipped)
+  int x_type[NXT];             // PS_GEOM_NONE / BOX / HULL
+  float x_pos[NXT][3], x_Q[NXT][9], x_hs[NXT][3], x_rb[NXT];
+  int x_v0[NXT], x_nv[NXT];    // hull vertices [x_v0, x_v0 + x_nv) of hull_v
+  int nxpairs;                 // hand-hand pairs with an extra collider: a | b << 8
+  int xpair[PS_MAX_XPAIRS];
+  alignas(16) float hull_v[NH * PS_HAND_HULLVERT][4];  // geom frame (w unused)
   // triangular (a,b) table for the LDL update
   int tri_a[NTRI + 8], tri_b[NTRI + 8];
   // v2 lane-owned topology (packed, loaded into registers once per launch)

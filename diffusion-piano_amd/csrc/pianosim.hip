@@ -17,6 +17,7 @@
 
 #include "devmodel.h"
 #include "prims.h"
+#include "collide_x.h"
 
 using namespace ps;
 
@@ -53,6 +54,8 @@ struct ps_env {
   int* episode;             // resets so far per env (the draw counter)
   int* stats;               // [N][PS_NSTATS] solver / cap counters of the last step
   uint64_t seed;
+  bool has_x;               // box / hull colliders: the pianosim_kernel<true> instantiation
+  Contact* con_out;         // [N][MAXCON] contact lists of the last step (ps_record_contacts)
 };
 
 static void quat2mat_h(const double* q, float* R) {
@@ -259,6 +262,16 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
   for (int h = 0; h < NH; h++)
     for (int g = 0; g < NG; g++) {
       int G = h * NG + g;
+      if (d->geom_body[h][g] >= NB) return fail("capsule body out of range");
+      if (d->geom_body[h][g] < 0) {
+        // unused slot: a point at the hand root with radius -1, whose inverted AABB never
+        // overlaps a key or the base; no capsule pair may name it
+        m->geom_body[G] = h * NB;
+        for (int i = 0; i < 3; i++) { m->geom_pos[G][i] = 0.f; m->geom_axis[G][i] = i == 2 ? 1.f : 0.f; }
+        m->geom_hl[G] = 0.f;
+        m->geom_r[G] = -1.f;
+        continue;
+      }
       m->geom_body[G] = h * NB + d->geom_body[h][g];
       for (int i = 0; i < 3; i++) {
         m->geom_pos[G][i] = (float)d->geom_pos[h][g][i];
@@ -267,6 +280,56 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       m->geom_hl[G] = (float)d->geom_halflen[h][g];
       m->geom_r[G] = (float)d->geom_radius[h][g];
     }
+  m->nx = 0;
+  for (int h = 0; h < NH; h++)
+    for (int i = 0; i < NX; i++) {
+      const int e = h * NX + i, t = d->xgeom_type[h][i];
+      m->x_type[e] = t;
+      m->geom_body[NGT + e] = h * NB;
+      if (t == PS_GEOM_NONE) continue;
+      if (t != PS_GEOM_BOX && t != PS_GEOM_HULL) return fail("unknown extra collider type");
+      if (d->xgeom_body[h][i] < 0 || d->xgeom_body[h][i] >= NB) return fail("extra collider body out of range");
+      m->nx++;
+      m->geom_body[NGT + e] = h * NB + d->xgeom_body[h][i];
+      double q[4], qn = 0;
+      for (int k = 0; k < 4; k++) { q[k] = d->xgeom_quat[h][i][k]; qn += q[k] * q[k]; }
+      if (!(qn > 0)) return fail("extra collider quaternion is zero");
+      qn = 1.0 / sqrt(qn);
+      for (int k = 0; k < 4; k++) q[k] *= qn;
+      const double w = q[0], x = q[1], y = q[2], z = q[3];
+      const double R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                           2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                           2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+      for (int k = 0; k < 9; k++) m->x_Q[e][k] = (float)R[k];
+      for (int k = 0; k < 3; k++) {
+        m->x_pos[e][k] = (float)d->xgeom_pos[h][i][k];
+        m->x_hs[e][k] = (float)d->xgeom_size[h][i][k];
+      }
+      m->x_rb[e] = (float)d->xgeom_rbound[h][i];
+      m->x_v0[e] = h * PS_HAND_HULLVERT + d->xgeom_vert[h][i][0];
+      m->x_nv[e] = d->xgeom_vert[h][i][1];
+      if (t == PS_GEOM_HULL && (d->xgeom_vert[h][i][0] < 0 || d->xgeom_vert[h][i][1] < 4 ||
+                                d->xgeom_vert[h][i][1] > PS_HULL_MAXVERT ||
+                                d->xgeom_vert[h][i][0] + d->xgeom_vert[h][i][1] > PS_HAND_HULLVERT))
+        return fail("hull vertex range out of bounds (4 .. PS_HULL_MAXVERT vertices)");
+      if (t == PS_GEOM_BOX && !(d->xgeom_size[h][i][0] > 0 && d->xgeom_size[h][i][1] > 0 && d->xgeom_size[h][i][2] > 0))
+        return fail("box half sizes must be positive");
+    }
+  for (int h = 0; h < NH; h++)
+    for (int v = 0; v < PS_HAND_HULLVERT; v++) {
+      for (int k = 0; k < 3; k++) m->hull_v[h * PS_HAND_HULLVERT + v][k] = (float)d->hull_vert[h][v][k];
+      m->hull_v[h * PS_HAND_HULLVERT + v][3] = 0.f;
+    }
+  if (d->n_xpairs < 0 || d->n_xpairs > PS_MAX_XPAIRS) return fail("bad n_xpairs");
+  m->nxpairs = d->n_xpairs;
+  for (int i = 0; i < d->n_xpairs; i++) {
+    const int a = d->xpair[i][0], b = d->xpair[i][1];
+    if (a < 0 || b < 0 || a >= NCOLL || b >= NCOLL || a >= b || b < NGT) return fail("extra pair index out of range");
+    if ((a < NGT && m->geom_r[a] < 0.f) || (a >= NGT && m->x_type[a - NGT] == PS_GEOM_NONE) ||
+        m->x_type[b - NGT] == PS_GEOM_NONE)
+      return fail("extra pair names an unused collider");
+    m->xpair[i] = a | (b << 8);
+  }
   m->root_geom_count = d->root_geom_count;
   // v2 packed lane topology + conservative piano prefilter bounds
   for (int B = 0; B < NBT; B++) {
@@ -335,6 +398,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     m->pair[i][1] = d->cappair[i][1];
     if (m->pair[i][0] < 0 || m->pair[i][0] >= NGT || m->pair[i][1] < 0 || m->pair[i][1] >= NGT)
       return fail("capsule pair index out of range");
+    if (m->geom_r[m->pair[i][0]] < 0.f || m->geom_r[m->pair[i][1]] < 0.f) return fail("capsule pair names an unused slot");
   }
   // the cross-hand pairs can be skipped wholesale when the hands' boxes are apart, if they
   // all come after the same-hand ones (model.capsule_pairs orders them so)
@@ -377,11 +441,13 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipSetDevice(device));
   DevModel* hm = new DevModel;
   if (build_dev_model(model, hm)) { delete hm; return -1; }
+  const bool has_x = hm->nx > 0 || hm->nxpairs > 0;
   ps_env* E = new ps_env();
   E->n = n_envs;
   E->device = device;
   E->cfg = *cfg;
   E->obs_dim = ps_obs_dim(cfg);
+  E->has_x = has_x;
   E->T = song->T;
   size_t N = (size_t)n_envs;
   HIPCHK(hipMalloc(&E->d_model, sizeof(DevModel)));
@@ -446,6 +512,7 @@ void ps_destroy(ps_env* E) {
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
   hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
   hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats);
+  if (E->con_out) hipFree(E->con_out);
   delete E;
 }
 
@@ -492,7 +559,7 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
           (uint32_t)E->seed, (uint32_t)(E->seed >> 32)};
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt,
-         E->hand_dy, E->episode, E->stats};
+         E->hand_dy, E->episode, E->stats, E->con_out};
   const int* order = nullptr;
   if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
     hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->stats, E->last, E->order,
@@ -500,8 +567,12 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
     HIPCHK(hipGetLastError());
     order = E->order;
   }
-  hipLaunchKernelGGL(pianosim_kernel, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b, action,
-                     mask, obs, reward, discount, step_type, mode, E->n, order);
+  if (E->has_x)
+    hipLaunchKernelGGL(pianosim_kernel<true>, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b,
+                       action, mask, obs, reward, discount, step_type, mode, E->n, order);
+  else
+    hipLaunchKernelGGL(pianosim_kernel<false>, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b,
+                       action, mask, obs, reward, discount, step_type, mode, E->n, order);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -622,6 +693,28 @@ int ps_set_hand_offset(ps_env* E, const float* dy, void* stream) {
   if (!E || !dy) return fail("null argument");
   if (!E->cfg.randomize_hand_positions) return fail("ps_set_hand_offset needs randomize_hand_positions");
   HIPCHK(hipMemcpyAsync(E->hand_dy, dy, sizeof(float) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+static_assert(sizeof(ps_contact) == sizeof(Contact), "ps_contact mirrors the kernel's contact record");
+int ps_record_contacts(ps_env* E, int on) {
+  if (!E) return fail("null argument");
+  if (on && !E->con_out) {
+    HIPCHK(hipSetDevice(E->device));
+    HIPCHK(hipMalloc(&E->con_out, sizeof(Contact) * MAXCON * (size_t)E->n));
+    HIPCHK(hipMemset(E->con_out, 0, sizeof(Contact) * MAXCON * (size_t)E->n));
+  } else if (!on && E->con_out) {
+    HIPCHK(hipFree(E->con_out));
+    E->con_out = nullptr;
+  }
+  return 0;
+}
+
+int ps_contacts(ps_env* E, ps_contact* out, void* stream) {
+  if (!E || !out) return fail("null argument");
+  if (!E->con_out) return fail("contact recording is off (ps_record_contacts)");
+  HIPCHK(hipMemcpyAsync(out, E->con_out, sizeof(Contact) * MAXCON * (size_t)E->n, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
   return 0;
 }
 

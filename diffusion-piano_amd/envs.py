@@ -289,6 +289,25 @@ class BatchedPianoEnv:
         _lib.check(_lib.load().ps_contact_count(self._h, t.data_ptr(), self.stream))
         return t
 
+    def record_contacts(self, on: bool = True) -> None:
+        """Keep each step's contact list for contacts() (ps_record_contacts; off by default)."""
+        _lib.check(_lib.load().ps_record_contacts(self._h, 1 if on else 0))
+
+    def contacts(self):
+        """-> list per env of (kind, key, g1, g2, dist, pos[3], normal[3]) of the last step's
+        task-layer collision pass (physics.data.contact); needs record_contacts()."""
+        raw = self._torch.empty(self.num_envs, abi.MAX_CONTACTS_LIMIT, 17, device=self.device, dtype=self._torch.float32)
+        _lib.check(_lib.load().ps_contacts(self._h, raw.data_ptr(), self.stream))
+        self._torch.cuda.synchronize(self.device)
+        f = raw.cpu().numpy()
+        ints = f.view(np.int32)
+        n = self.contact_count().cpu().numpy()
+        out = []
+        for e in range(self.num_envs):
+            out.append([(int(ints[e, c, 13]), int(ints[e, c, 14]), int(ints[e, c, 15]), int(ints[e, c, 16]),
+                         float(f[e, c, 12]), f[e, c, 0:3].copy(), f[e, c, 3:6].copy()) for c in range(n[e])])
+        return out
+
     def musical_metrics(self):
         """-> (episode [N, 6] f32, episodes [N] i32): each env's last finished episode's mean
         precision / recall / F1 / sustain_precision / sustain_recall / sustain_f1

@@ -17,15 +17,21 @@ The supported subset is what the hot path simulates:
 * ``<joint type=hinge|slide axis range damping armature>``, and ``stiffness`` must be 0;
 * ``<geom>`` colliders (contype or conaffinity non-zero): capsules (``size`` + frame, or
   ``fromto``) and cylinders, which become capsules as in the reference's MJX path
-  (parallelized_base.py:49-64). Non-colliding (visual) geoms are skipped. Any other
-  collider type raises ``ValueError``, because the kernel has no mesh/box hand colliders;
+  (parallelized_base.py:49-64); boxes (``size`` = half sizes); meshes, which collide as the
+  convex hull of their vertices as in MuJoCo (``<asset><mesh file=... scale=...>`` with an
+  OBJ or STL file under ``<compiler meshdir>``, or inline ``vertex=``; the hull is computed
+  with qhull, MuJoCo's hull library, and centred at its volume centroid, MuJoCo's mesh
+  frame origin; at most ``abi.HULL_MAXVERT`` hull vertices). Non-colliding (visual) geoms
+  are skipped; spheres, ellipsoids, planes and primitives fitted to a mesh raise
+  ``ValueError``;
 * ``<tendon><fixed>`` over two joints;
 * ``<actuator><position joint|tendon kp ctrlrange forcerange>``;
 * ``<contact><exclude body1 body2>``.
 
 The ABI fixes the hand's sizes (``abi.HAND_NBODY`` bodies, ``HAND_NDOF`` - 2 joints,
-``HAND_NGEOM`` capsules, ``HAND_NACT`` - 2 actuators, ``HAND_NTENDON`` tendons), and a
-model that differs raises ``ValueError`` naming the count.
+``HAND_NACT`` - 2 actuators, ``HAND_NTENDON`` tendons; at most ``HAND_NGEOM`` capsules and
+``HAND_NXGEOM`` box / mesh colliders), and a model that differs raises ``ValueError`` naming
+the count.
 """
 
 from __future__ import annotations
@@ -162,6 +168,45 @@ def _mat_quat(R):
     return tuple(q)
 
 
+def _mesh_vertices(path: Path) -> np.ndarray:
+    """Vertices of an OBJ (``v`` lines) or STL (binary or ASCII) file."""
+    data = path.read_bytes()
+    suffix = path.suffix.lower()
+    if suffix == ".obj":
+        rows = [ln.split()[1:4] for ln in data.decode("utf-8", "replace").splitlines() if ln.startswith("v ")]
+        return np.asarray(rows, dtype=np.float64).reshape(-1, 3)
+    if suffix == ".stl":
+        if data[:5].lower() == b"solid" and b"facet" in data[:2048]:
+            rows = [ln.split()[1:4] for ln in data.decode("utf-8", "replace").splitlines()
+                    if ln.strip().startswith("vertex")]
+            return np.asarray(rows, dtype=np.float64).reshape(-1, 3)
+        n = int(np.frombuffer(data[80:84], dtype="<u4")[0])
+        rec = np.frombuffer(data[84:84 + 50 * n], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)),
+                                                                  ("a", "<u2")]))
+        return rec["v"].reshape(-1, 3).astype(np.float64)
+    raise ValueError(f"mesh file {path.name!r}: only .obj and .stl are supported")
+
+
+def convex_hull_collider(points) -> Tuple[np.ndarray, np.ndarray]:
+    """(centre, hull vertices relative to it) of a point set: qhull's convex hull, centred at
+    the hull's volume centroid."""
+    from scipy.spatial import ConvexHull  # qhull, the library MuJoCo computes mesh hulls with
+
+    pts = np.asarray(points, dtype=np.float64)
+    hull = ConvexHull(pts)
+    verts = pts[hull.vertices]
+    # volume centroid: tetrahedra from an interior point to every facet
+    o = verts.mean(axis=0)
+    vol, cen = 0.0, np.zeros(3)
+    for f in hull.simplices:
+        a, b, c = pts[f[0]] - o, pts[f[1]] - o, pts[f[2]] - o
+        v = abs(np.dot(a, np.cross(b, c))) / 6.0
+        vol += v
+        cen += v * (a + b + c) / 4.0
+    centre = o + cen / vol
+    return centre, verts - centre
+
+
 def _strip(name: Optional[str], prefix: str) -> Optional[str]:
     if name is not None and prefix and name.startswith(prefix):
         return name[len(prefix):]
@@ -178,6 +223,27 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     if root.tag != "mujoco":
         raise ValueError("not an MJCF document (root element is not <mujoco>)")
     ctx = _Ctx(root)
+    base_dir = Path(source).parent if not (isinstance(source, str) and source.lstrip().startswith("<")) else Path(".")
+    comp = root.find("compiler")
+    mesh_dir = base_dir / (comp.get("meshdir", comp.get("assetdir", "")) if comp is not None else "")
+    meshes: Dict[str, ET.Element] = {}
+    for asset in root.findall("asset"):
+        for me in asset.findall("mesh"):
+            mname = me.get("name") or Path(me.get("file", "")).stem
+            meshes[mname] = me
+
+    def mesh_points(mname: str) -> np.ndarray:
+        me = meshes.get(mname)
+        if me is None:
+            raise ValueError(f"unknown mesh {mname!r}")
+        if me.get("vertex"):
+            pts = np.asarray(_floats(me.get("vertex")), dtype=np.float64).reshape(-1, 3)
+        elif me.get("file"):
+            pts = _mesh_vertices(mesh_dir / me.get("file"))
+        else:
+            raise ValueError(f"mesh {mname!r} has neither file= nor vertex=")
+        return pts * np.asarray(_floats(me.get("scale", "1 1 1")), dtype=np.float64)
+
     wb = root.find("worldbody")
     roots = [] if wb is None else wb.findall("body")
     if len(roots) != 1:
@@ -186,6 +252,7 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     bodies: List[M.Body] = []
     dofs: List[M.Dof] = []
     geoms: List[M.Geom] = []
+    xgeoms: List[M.XGeom] = []
     body_idx: Dict[str, int] = {}
     joint_idx: Dict[str, int] = {}
     root_joint_attrs: Dict[str, str] = {}
@@ -243,10 +310,29 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
             if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
                 continue  # visual only
             gtype = ga.get("type", "sphere")
-            if gtype not in ("capsule", "cylinder"):
+            if gtype not in ("capsule", "cylinder", "box", "mesh"):
                 raise ValueError(f"body {name!r}: collider type {gtype!r} is not supported "
-                                 "(capsule/cylinder; the kernel has no mesh or box hand colliders)")
+                                 "(capsule/cylinder, box, mesh)")
+            if gtype != "mesh" and "mesh" in ga:
+                raise ValueError(f"body {name!r}: a {gtype} fitted to mesh {ga['mesh']!r} is not supported")
             size = _floats(ga.get("size", "0"))
+            if gtype == "box":
+                if len(size) < 3:
+                    raise ValueError(f"body {name!r}: box needs size='x y z' half sizes")
+                xgeoms.append(M.XGeom(bi, "box", tuple(_floats(ga.get("pos", "0 0 0"))),
+                                      tuple(ctx.frame_quat(ga)), tuple(size[:3])))
+                continue
+            if gtype == "mesh":
+                if "mesh" not in ga:
+                    raise ValueError(f"body {name!r}: mesh geom without mesh=")
+                centre, verts = convex_hull_collider(mesh_points(ga["mesh"]))
+                if len(verts) > abi.HULL_MAXVERT:
+                    raise ValueError(f"mesh {ga['mesh']!r}: convex hull has {len(verts)} vertices; "
+                                     f"at most {abi.HULL_MAXVERT} are supported")
+                q = M.quat_normalize(ctx.frame_quat(ga))
+                gpos = np.asarray(_floats(ga.get("pos", "0 0 0"))) + M.quat_to_mat(q) @ centre
+                xgeoms.append(M.XGeom(bi, "hull", tuple(gpos), tuple(q), verts=verts))
+                continue
             if "fromto" in ga:
                 ft = np.asarray(_floats(ga["fromto"]), np.float64)
                 p0, p1 = ft[:3], ft[3:]
@@ -332,11 +418,14 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     obs_order = [remap[i] for i in range(n_menagerie_joints)] + [n_root + i for i in range(len(slides))]
 
     for what, got, want in (("bodies", len(bodies), abi.HAND_NBODY), ("joints", len(dofs), abi.HAND_NDOF),
-                            ("capsule colliders", len(geoms), abi.HAND_NGEOM),
                             ("actuators", len(acts), abi.HAND_NACT), ("fixed tendons", len(tendons), abi.HAND_NTENDON)):
         if got != want:
             raise ValueError(f"hand has {got} {what} (with the forearm DOFs); the kernel ABI needs {want}")
-    return M.HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order, tcoef)
+    for what, got, most in (("capsule/cylinder colliders", len(geoms), abi.HAND_NGEOM),
+                            ("box/mesh colliders", len(xgeoms), abi.HAND_NXGEOM)):
+        if got > most:
+            raise ValueError(f"hand has {got} {what}; the kernel ABI holds at most {most}")
+    return M.HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order, tcoef, xgeoms or None)
 
 
 # ------------------------------------------------------------------ writer
@@ -362,6 +451,11 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
     ET.SubElement(ET.SubElement(hand, "default", {"class": "plastic_visual"}), "geom", type="mesh",
                   contype="0", conaffinity="0", group="2")
 
+    if spec.xgeoms:
+        assets = ET.SubElement(root, "asset")
+        for j, xg in enumerate(spec.xgeoms):
+            if xg.kind == "hull":
+                ET.SubElement(assets, "mesh", name=f"hull{j}", vertex=_fmt(np.asarray(xg.verts).ravel()))
     names = {i: b.name for i, b in enumerate(spec.bodies)}
     els: Dict[int, ET.Element] = {}
     wb = ET.SubElement(root, "worldbody")
@@ -403,6 +497,15 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
             else:
                 ET.SubElement(el, "geom", {"class": "plastic_collision", "size": _fmt((g.radius, g.halflen)),
                                            "pos": _fmt(g.pos), "quat": _fmt(_quat_from_z(g.axis))})
+        for j, xg in enumerate(spec.xgeoms or []):
+            if xg.body != i:
+                continue
+            if xg.kind == "box":
+                ET.SubElement(el, "geom", {"class": "plastic_collision", "type": "box", "size": _fmt(xg.size),
+                                           "pos": _fmt(xg.pos), "quat": _fmt(xg.quat)})
+            else:
+                ET.SubElement(el, "geom", {"class": "plastic_collision", "type": "mesh", "mesh": f"hull{j}",
+                                           "pos": _fmt(xg.pos), "quat": _fmt(xg.quat)})
     cont = ET.SubElement(root, "contact")
     for a, b in spec.excludes:
         ET.SubElement(cont, "exclude", body1=prefix + names[a], body2=prefix + names[b])

@@ -153,6 +153,24 @@ class Geom:
     radius: float
 
 
+@dataclass
+class XGeom:
+    """A box or convex-hull collider (MuJoCo geom type box / mesh). ``pos``/``quat``: geom
+    frame in the body frame; box: ``size`` = half sizes; hull: ``verts`` in the geom frame,
+    whose origin is the hull's centre (MuJoCo re-centres a mesh at its centroid)."""
+    body: int
+    kind: str                                   # "box" | "hull"
+    pos: Tuple[float, float, float]
+    quat: Tuple[float, float, float, float] = (1.0, 0.0, 0.0, 0.0)
+    size: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+    verts: Optional[np.ndarray] = None          # [n, 3], hull only
+
+    def rbound(self) -> float:
+        if self.kind == "box":
+            return float(np.linalg.norm(self.size))
+        return float(np.max(np.linalg.norm(np.asarray(self.verts, dtype=np.float64), axis=1)))
+
+
 class HandSpec(NamedTuple):
     """One (right) hand as build_model consumes it: the authored tree below, or a user MJCF
     through ``mjcf.load_hand``. Indices are MuJoCo's: bodies in depth-first document order,
@@ -167,6 +185,7 @@ class HandSpec(NamedTuple):
     acts: List[tuple]                          # (kind 0 joint / 1 tendon, target, kp, ctrlrange, forcerange|None)
     obs_order: List[int]                       # joints_pos observation order (dof indices)
     tendon_coef: Optional[List[Tuple[float, float]]] = None  # None = (1, 1) each
+    xgeoms: Optional[List[XGeom]] = None       # box / hull colliders beside the capsules
 
 
 ID = (1.0, 0.0, 0.0, 0.0)
@@ -415,6 +434,8 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
             m.dof_damping[h][j] = damping
             m.dof_armature[h][j] = dof.armature
             m.dof_obs_order[h][j] = obs_order[j]
+        for g in range(abi.HAND_NGEOM):
+            m.geom_body[h][g] = -1  # unused slot
         for g, geom in enumerate(geoms):
             m.geom_body[h][g] = geom.body
             m.geom_pos[h][g][:] = _mirror_vec(geom.pos) if mir else geom.pos
@@ -436,12 +457,43 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
             m.act_ctrlrange[h][a][:] = cr
             m.act_forcelimited[h][a] = 0 if fr is None else 1
             m.act_forcerange[h][a][:] = (0.0, 0.0) if fr is None else fr
+    xgeoms = spec.xgeoms or []
+    if len(geoms) > abi.HAND_NGEOM or len(xgeoms) > abi.HAND_NXGEOM:
+        raise ValueError(f"at most {abi.HAND_NGEOM} capsule and {abi.HAND_NXGEOM} box/hull colliders per hand "
+                         f"(got {len(geoms)} and {len(xgeoms)})")
+    for h in range(abi.NHAND):
+        mir = h == 1
+        nv = 0
+        for i, xg in enumerate(xgeoms):
+            m.xgeom_type[h][i] = abi.GEOM_BOX if xg.kind == "box" else abi.GEOM_HULL
+            m.xgeom_body[h][i] = xg.body
+            m.xgeom_pos[h][i][:] = _mirror_vec(xg.pos) if mir else xg.pos
+            q = quat_normalize(xg.quat)
+            m.xgeom_quat[h][i][:] = _mirror_quat(q) if mir else q
+            m.xgeom_size[h][i][:] = xg.size
+            m.xgeom_rbound[h][i] = xg.rbound()
+            if xg.kind == "hull":
+                v = np.asarray(xg.verts, dtype=np.float64)
+                if not 4 <= len(v) <= abi.HULL_MAXVERT:
+                    raise ValueError(f"a hull collider needs 4..{abi.HULL_MAXVERT} vertices, got {len(v)}")
+                if nv + len(v) > abi.HAND_HULLVERT:
+                    raise ValueError(f"more than {abi.HAND_HULLVERT} hull vertices in one hand")
+                m.xgeom_vert[h][i][:] = (nv, len(v))
+                for j, p in enumerate(v):
+                    m.hull_vert[h][nv + j][:] = _mirror_vec(p) if mir else p
+                nv += len(v)
     set_const(m)
     pairs = capsule_pairs(bodies, geoms, excludes) if hand_collisions else []
     assert len(pairs) <= abi.MAX_CAPPAIRS
     m.n_cappairs = len(pairs)
     for i, (a, b) in enumerate(pairs):
         m.cappair[i][:] = (a, b)
+    xpairs = extra_pairs(bodies, geoms, xgeoms, excludes) if hand_collisions else []
+    if len(xpairs) > abi.MAX_XPAIRS:
+        raise ValueError(f"{len(xpairs)} collider pairs with a box/hull collider; at most {abi.MAX_XPAIRS}")
+    m.n_xpairs = len(xpairs)
+    for i, (a, b) in enumerate(xpairs):
+        m.xpair[i][:] = (a, b)
     return m
 
 
@@ -519,7 +571,7 @@ def capsule_pairs(bodies, geoms, excludes):
     """
     ex = {frozenset(p) for p in excludes}
     pairs = []
-    ng = len(geoms)
+    ng, stride = len(geoms), abi.HAND_NGEOM  # global id h * HAND_NGEOM + g (unused slots past ng)
     for h in range(abi.NHAND):
         for a in range(ng):
             for b in range(a + 1, ng):
@@ -528,10 +580,34 @@ def capsule_pairs(bodies, geoms, excludes):
                     continue
                 if frozenset((ba, bb)) in ex:
                     continue
-                pairs.append((h * ng + a, h * ng + b))
+                pairs.append((h * stride + a, h * stride + b))
     for a in range(ng):
         for b in range(ng):
-            pairs.append((a, ng + b))
+            pairs.append((a, stride + b))
+    return pairs
+
+
+def extra_pairs(bodies, geoms, xgeoms, excludes):
+    """Hand-hand collider pairs with at least one box/hull collider, MuJoCo-filtered as
+    capsule_pairs, in global ids (capsule h*HAND_NGEOM + g, extra 2*HAND_NGEOM +
+    h*HAND_NXGEOM + i), ordered by (a, b) with a < b."""
+    ex = {frozenset(p) for p in excludes}
+    ng, nx = abi.HAND_NGEOM, abi.HAND_NXGEOM
+    coll = []  # (global id, hand, body, is_extra)
+    for h in range(abi.NHAND):
+        coll += [(h * ng + g, h, geom.body, False) for g, geom in enumerate(geoms)]
+    for h in range(abi.NHAND):
+        coll += [(abi.NHAND * ng + h * nx + i, h, xg.body, True) for i, xg in enumerate(xgeoms)]
+    coll.sort()
+    pairs = []
+    for ia, (ga, ha, ba, xa) in enumerate(coll):
+        for gb, hb, bb, xb in coll[ia + 1:]:
+            if not (xa or xb):
+                continue
+            if ha == hb:
+                if ba == bb or bodies[ba].parent == bb or bodies[bb].parent == ba or frozenset((ba, bb)) in ex:
+                    continue
+            pairs.append((ga, gb))
     return pairs
 
 

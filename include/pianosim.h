@@ -56,6 +56,16 @@ extern "C" {
 #define PS_NU (PS_NHAND * PS_HAND_NACT)               /* 44 */
 #define PS_NACTION (PS_NU + 1)                        /* 45: hands + sustain */
 #define PS_MAX_CAPPAIRS 768 /* capsule-capsule candidate pairs after filtering */
+/* Box and convex-hull hand colliders ("extra" geoms, beside the capsule slots): MuJoCo geom
+ * types box and mesh (the Menagerie hand's palm boxes and distal meshes, shadow_hand.py:95,
+ * 144-152). A mesh collides as the convex hull of its vertices, as in MuJoCo. */
+#define PS_HAND_NXGEOM 12      /* extra colliders per hand */
+#define PS_HULL_MAXVERT 64     /* vertices of one hull */
+#define PS_HAND_HULLVERT 384   /* hull vertices per hand, all hulls */
+#define PS_MAX_XPAIRS 1024     /* hand-hand candidate pairs that involve an extra collider */
+#define PS_GEOM_NONE 0
+#define PS_GEOM_BOX 1
+#define PS_GEOM_HULL 2
 #define PS_MAX_NOTES 16     /* notes per control step in the song tables */
 
 /* Per-geom contact parameters (MuJoCo geom attributes). */
@@ -101,13 +111,14 @@ typedef struct {
   double dof_damping[PS_NHAND][PS_HAND_NDOF];
   double dof_armature[PS_NHAND][PS_HAND_NDOF];
   int32_t dof_obs_order[PS_NHAND][PS_HAND_NDOF]; /* joints_pos[i] = qpos[dof_obs_order[i]] */
-  /* capsule colliders (body frame segment centre/axis) */
+  /* capsule colliders (body frame segment centre/axis); geom_body < 0: unused slot */
   int32_t geom_body[PS_NHAND][PS_HAND_NGEOM];
   double geom_pos[PS_NHAND][PS_HAND_NGEOM][3];
   double geom_axis[PS_NHAND][PS_HAND_NGEOM][3];
   double geom_halflen[PS_NHAND][PS_HAND_NGEOM];
   double geom_radius[PS_NHAND][PS_HAND_NGEOM];
-  int32_t root_geom_count;   /* geoms [0, root_geom_count) belong to the root (forearm) body */
+  int32_t root_geom_count;   /* capsules [0, root_geom_count) belong to the root (forearm) body
+                                (informational: the forearm reward tests the bodies) */
   ps_contact_param hand_contact;
   /* fingertip sites (shadow_hand.py:190-207) */
   int32_t site_body[PS_NHAND][PS_NFINGER];
@@ -132,6 +143,23 @@ typedef struct {
   double key_dof_invweight[PS_NKEY];
   double body_invweight[PS_NHAND][PS_HAND_NBODY];
   double dof_invweight[PS_NHAND][PS_HAND_NDOF];
+  /* extra colliders (type PS_GEOM_NONE = unused slot). Frame in the body frame; box: half
+   * sizes; hull: vertices [xgeom_vert[0], +xgeom_vert[1]) of hull_vert in the geom frame,
+   * whose origin is the hull's centre (MuJoCo's mesh frame). rbound: bounding-sphere radius
+   * about the geom origin. Global collider ids: capsule h*PS_HAND_NGEOM + g, extra
+   * PS_NHAND*PS_HAND_NGEOM + h*PS_HAND_NXGEOM + i. */
+  int32_t xgeom_type[PS_NHAND][PS_HAND_NXGEOM];
+  int32_t xgeom_body[PS_NHAND][PS_HAND_NXGEOM];
+  double xgeom_pos[PS_NHAND][PS_HAND_NXGEOM][3];
+  double xgeom_quat[PS_NHAND][PS_HAND_NXGEOM][4];
+  double xgeom_size[PS_NHAND][PS_HAND_NXGEOM][3];
+  double xgeom_rbound[PS_NHAND][PS_HAND_NXGEOM];
+  int32_t xgeom_vert[PS_NHAND][PS_HAND_NXGEOM][2];
+  double hull_vert[PS_NHAND][PS_HAND_HULLVERT][3];
+  /* hand-hand candidate pairs with at least one extra collider (a < b, global ids), after
+   * MuJoCo's filtering; contacts of these follow the capsule-capsule ones */
+  int32_t n_xpairs;
+  int32_t xpair[PS_MAX_XPAIRS][2];
 } ps_model_desc;
 
 /* Song tables: NoteTrajectory in dense form (music.py:SongTables). */
@@ -237,6 +265,21 @@ int ps_reward_terms(ps_env* env, float* terms, void* stream);
 int ps_fingertips(ps_env* env, float* xpos, void* stream);
 /* Number of contacts after the last step/reset, [N]. */
 int ps_contact_count(ps_env* env, int32_t* ncon, void* stream);
+
+/* One contact of the task layer's final collision pass (physics.data.contact after the step):
+ * position (world), frame (normal geom1 -> geom2, two tangents), signed distance (< 0:
+ * penetration), kind (0 hand-key, 1 hand-base, 2 hand-hand), key index (kind 0), global
+ * collider ids g1 (-1 for a key or the base) and g2. */
+typedef struct {
+  float pos[3], n[3], t1[3], t2[3], dist;
+  int32_t kind, key, g1, g2;
+} ps_contact;
+/* Contact lists of each env's last step: ps_record_contacts(env, 1) makes the step kernel
+ * keep them (off by default: ~70 B per contact of extra HBM writes); ps_contacts copies them
+ * to out [N][PS_MAX_CONTACTS_LIMIT] (device; the first ncon of each env are valid). No
+ * reference counterpart beyond physics.data.contact; used for collision parity checks. */
+int ps_record_contacts(ps_env* env, int on);
+int ps_contacts(ps_env* env, ps_contact* out, void* stream);
 
 /* Musical metrics of each env's LAST finished episode, [N][PS_NMUSIC] (per-step binary
  * precision / recall / F1 with zero_division = 1, as sklearn's precision_recall_fscore_support

@@ -37,6 +37,8 @@
 #define ND PS_HAND_NDOF
 #define NG PS_HAND_NGEOM
 #define NA PS_HAND_NACT
+#define NX PS_HAND_NXGEOM
+#define NCAPS (NH * NG)  /* global collider ids: capsules [0, NCAPS), extras NCAPS + h * NX + i */
 #define NV PS_NV
 #define MAXCON PS_MAX_CONTACTS_LIMIT
 #define MAXROW (4 * MAXCON + NH * ND * 2 + NK)  /* storage; coupled rows are capped at PS_MAX_ROWS */
@@ -157,6 +159,8 @@ typedef struct {
   v3 o[NH][NB], com[NH][NB], axis[NH][ND];
   double Iw[NH][NB][9];
   v3 cap0[NH][NG], cap1[NH][NG];
+  v3 xc[NH][NX];   /* extra colliders: world frame origin and rotation */
+  m3 xR[NH][NX];
   m3 keyR[NK];
   v3 keyc[NK], keyanchor[NK];
   /* dynamics */
@@ -259,10 +263,17 @@ static void kinematics(const model* m, envdata* E) {
     }
     for (int g = 0; g < NG; g++) {
       int b = d->geom_body[h][g];
+      if (b < 0) continue;  /* unused slot */
       v3 c = add(E->o[h][b], mv(E->R[h][b], mk(d->geom_pos[h][g][0], d->geom_pos[h][g][1], d->geom_pos[h][g][2])));
       v3 a = mv(E->R[h][b], mk(d->geom_axis[h][g][0], d->geom_axis[h][g][1], d->geom_axis[h][g][2]));
       E->cap0[h][g] = sub(c, scl(a, d->geom_halflen[h][g]));
       E->cap1[h][g] = add(c, scl(a, d->geom_halflen[h][g]));
+    }
+    for (int i = 0; i < NX; i++) {
+      if (d->xgeom_type[h][i] == PS_GEOM_NONE) continue;
+      int b = d->xgeom_body[h][i];
+      E->xc[h][i] = add(E->o[h][b], mv(E->R[h][b], mk(d->xgeom_pos[h][i][0], d->xgeom_pos[h][i][1], d->xgeom_pos[h][i][2])));
+      E->xR[h][i] = mm(E->R[h][b], quat2mat(d->xgeom_quat[h][i]));
     }
   }
   for (int k = 0; k < NK; k++) {
@@ -604,6 +615,365 @@ static void seg_seg(v3 p1, v3 q1, v3 p2, v3 q2, v3* c1, v3* c2) {
   *c2 = add(p2, scl(d2, t));
 }
 
+/* ---------------------------------------------- box and convex-hull colliders
+ * A collider in world coordinates for the narrow phases below: capsule (segment p0-p1,
+ * radius r), box (centre c, rotation R, half sizes hs) or convex hull (centre c = the geom
+ * origin, rotation R, vertices in the geom frame). */
+typedef struct {
+  int type;            /* 0 capsule, PS_GEOM_BOX, PS_GEOM_HULL */
+  v3 c;
+  m3 R;
+  v3 p0, p1;
+  double r;
+  double hs[3];
+  const double (*vert)[3];
+  int nvert;
+} shape;
+
+static double sgn0(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
+
+/* support point of the shape in direction d (MuJoCo's mjccd_support: box corner by the sign
+ * of each local component, 0 on a zero component; capsule end by the sign along the axis
+ * plus the radius along d; hull: first vertex of maximal projection) */
+static v3 support(const shape* s, v3 d) {
+  if (s->type == 0) {
+    v3 ax = sub(s->p1, s->p0);
+    double dn = nrm(d);
+    v3 base = dot(ax, d) >= 0.0 ? s->p1 : s->p0;
+    if (dot(ax, d) == 0.0) base = scl(add(s->p0, s->p1), 0.5);
+    return dn > 0.0 ? add(base, scl(d, s->r / dn)) : base;
+  }
+  v3 dl = mtv(s->R, d);
+  v3 loc;
+  if (s->type == PS_GEOM_BOX) {
+    loc = mk(sgn0(dl.v[0]) * s->hs[0], sgn0(dl.v[1]) * s->hs[1], sgn0(dl.v[2]) * s->hs[2]);
+  } else {
+    int best = 0;
+    double bd = -INFINITY;
+    for (int i = 0; i < s->nvert; i++) {
+      double p = dl.v[0] * s->vert[i][0] + dl.v[1] * s->vert[i][1] + dl.v[2] * s->vert[i][2];
+      if (p > bd) { bd = p; best = i; }
+    }
+    loc = mk(s->vert[best][0], s->vert[best][1], s->vert[best][2]);
+  }
+  return add(s->c, mv(s->R, loc));
+}
+
+static v3 shape_centre(const shape* s) { return s->type == 0 ? scl(add(s->p0, s->p1), 0.5) : s->c; }
+
+/* Minkowski portal refinement (Snethen, GPG7 2.5), the penetration query of libccd's
+ * ccdMPRPenetration that MuJoCo's convex collider mjc_Convex runs for mesh geoms (one
+ * contact per pair; tolerance 1e-6, at most 50 refinements as MuJoCo's defaults). Portal
+ * points are supports of the difference A - B, kept with their A and B witnesses. Returns 1
+ * with depth >= 0, the normal A -> B and the contact point (midpoint of the witnesses), or
+ * 0 when the shapes are apart. */
+#define MPR_TOL 1e-6
+#define MPR_MAXIT 50
+#define MPR_EPS 2.220446049250313e-16   /* libccd CCD_EPS (double build) */
+typedef struct { v3 v, a, b; } mpr_pt;
+
+static int mpr_zero(double x) { return fabs(x) < MPR_EPS; }
+static mpr_pt mpr_support(const shape* A, const shape* B, v3 d) {
+  mpr_pt p;
+  p.a = support(A, d);
+  p.b = support(B, scl(d, -1.0));
+  p.v = sub(p.a, p.b);
+  return p;
+}
+static v3 nrmz(v3 a) { double n = nrm(a); return n > 0.0 ? scl(a, 1.0 / n) : a; }
+static v3 portal_dir(const mpr_pt* P) { return nrmz(crs(sub(P[2].v, P[1].v), sub(P[3].v, P[1].v))); }
+static int portal_reach_tol(const mpr_pt* P, const mpr_pt* v4, v3 dir) {
+  double d4 = dot(v4->v, dir);
+  double m = fmin(d4 - dot(P[1].v, dir), fmin(d4 - dot(P[2].v, dir), d4 - dot(P[3].v, dir)));
+  return m <= MPR_TOL;
+}
+static void expand_portal(mpr_pt* P, const mpr_pt* v4) {
+  v3 v4v0 = crs(v4->v, P[0].v);
+  if (dot(P[1].v, v4v0) > 0.0) {
+    if (dot(P[2].v, v4v0) > 0.0) P[1] = *v4; else P[3] = *v4;
+  } else {
+    if (dot(P[3].v, v4v0) > 0.0) P[2] = *v4; else P[1] = *v4;
+  }
+}
+/* closest point of triangle (a, b, c) to the origin (Ericson, RTCD 5.1.5) */
+static v3 tri_closest_origin(v3 a, v3 b, v3 c) {
+  v3 ab = sub(b, a), ac = sub(c, a), ap = scl(a, -1.0);
+  double d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0.0 && d2 <= 0.0) return a;
+  v3 bp = scl(b, -1.0);
+  double d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0.0 && d4 <= d3) return b;
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) return add(a, scl(ab, d1 / (d1 - d3)));
+  v3 cp = scl(c, -1.0);
+  double d5 = dot(ab, cp), d6 = dot(ac, cp);
+  if (d6 >= 0.0 && d5 <= d6) return c;
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) return add(a, scl(ac, d2 / (d2 - d6)));
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0)
+    return add(b, scl(sub(c, b), (d4 - d3) / ((d4 - d3) + (d5 - d6))));
+  double den = 1.0 / (va + vb + vc);
+  return add(a, add(scl(ab, vb * den), scl(ac, vc * den)));
+}
+static v3 mpr_pos(const mpr_pt* P) {
+  v3 dir = portal_dir(P);
+  double b[4];
+  b[0] = dot(crs(P[1].v, P[2].v), P[3].v);
+  b[1] = dot(crs(P[3].v, P[2].v), P[0].v);
+  b[2] = dot(crs(P[0].v, P[1].v), P[3].v);
+  b[3] = dot(crs(P[2].v, P[1].v), P[0].v);
+  double sum = b[0] + b[1] + b[2] + b[3];
+  if (mpr_zero(sum) || sum < 0.0) {
+    b[0] = 0.0;
+    b[1] = dot(crs(P[2].v, P[3].v), dir);
+    b[2] = dot(crs(P[3].v, P[1].v), dir);
+    b[3] = dot(crs(P[1].v, P[2].v), dir);
+    sum = b[1] + b[2] + b[3];
+  }
+  double inv = 1.0 / sum;
+  v3 pa = mk(0, 0, 0), pb = mk(0, 0, 0);
+  for (int i = 0; i < 4; i++) { pa = add(pa, scl(P[i].a, b[i])); pb = add(pb, scl(P[i].b, b[i])); }
+  return scl(add(scl(pa, inv), scl(pb, inv)), 0.5);
+}
+static int mpr_penetration(const shape* A, const shape* B, double* depth, v3* n, v3* pos) {
+  mpr_pt P[4];
+  /* discover the portal */
+  P[0].a = shape_centre(A); P[0].b = shape_centre(B); P[0].v = sub(P[0].a, P[0].b);
+  if (P[0].v.v[0] == 0.0 && P[0].v.v[1] == 0.0 && P[0].v.v[2] == 0.0) P[0].v.v[0] += 10.0 * MPR_EPS;
+  v3 dir = nrmz(scl(P[0].v, -1.0));
+  P[1] = mpr_support(A, B, dir);
+  double dt = dot(P[1].v, dir);
+  if (mpr_zero(dt) || dt < 0.0) return 0;
+  dir = crs(P[0].v, P[1].v);
+  if (mpr_zero(dot(dir, dir))) {
+    if (P[1].v.v[0] == 0.0 && P[1].v.v[1] == 0.0 && P[1].v.v[2] == 0.0) {  /* touching at v1 */
+      *depth = 0.0; *n = mk(0, 0, 0); *pos = scl(add(P[1].a, P[1].b), 0.5);
+    } else {  /* the origin lies on the segment v0-v1 */
+      *pos = scl(add(P[1].a, P[1].b), 0.5);
+      *depth = nrm(P[1].v); *n = nrmz(P[1].v);
+    }
+    return 1;
+  }
+  dir = nrmz(dir);
+  P[2] = mpr_support(A, B, dir);
+  dt = dot(P[2].v, dir);
+  if (mpr_zero(dt) || dt < 0.0) return 0;
+  dir = nrmz(crs(sub(P[1].v, P[0].v), sub(P[2].v, P[0].v)));
+  if (dot(dir, P[0].v) > 0.0) { mpr_pt t = P[1]; P[1] = P[2]; P[2] = t; dir = scl(dir, -1.0); }
+  for (int it = 0;; it++) {
+    if (it > 4 * MPR_MAXIT) return 0;  /* guard (libccd has none here) */
+    P[3] = mpr_support(A, B, dir);
+    dt = dot(P[3].v, dir);
+    if (mpr_zero(dt) || dt < 0.0) return 0;
+    int cont = 0;
+    double t = dot(crs(P[1].v, P[3].v), P[0].v);
+    if (t < 0.0 && !mpr_zero(t)) { P[2] = P[3]; cont = 1; }
+    if (!cont) {
+      t = dot(crs(P[3].v, P[2].v), P[0].v);
+      if (t < 0.0 && !mpr_zero(t)) { P[1] = P[3]; cont = 1; }
+    }
+    if (!cont) break;
+    dir = nrmz(crs(sub(P[1].v, P[0].v), sub(P[2].v, P[0].v)));
+  }
+  /* refine until the portal contains the origin */
+  for (int it = 0;; it++) {
+    if (it > 4 * MPR_MAXIT) return 0;  /* guard */
+    dir = portal_dir(P);
+    dt = dot(P[1].v, dir);
+    if (mpr_zero(dt) || dt > 0.0) break;  /* portal encapsulates the origin */
+    mpr_pt v4 = mpr_support(A, B, dir);
+    double d4 = dot(v4.v, dir);
+    if (!(mpr_zero(d4) || d4 > 0.0) || portal_reach_tol(P, &v4, dir)) return 0;
+    expand_portal(P, &v4);
+  }
+  /* penetration: refine toward the boundary, then the portal's distance to the origin */
+  for (int it = 0;; it++) {
+    dir = portal_dir(P);
+    mpr_pt v4 = mpr_support(A, B, dir);
+    if (portal_reach_tol(P, &v4, dir) || it > MPR_MAXIT) {
+      v3 cp = tri_closest_origin(P[1].v, P[2].v, P[3].v);
+      *depth = nrm(cp);
+      *n = mpr_zero(*depth) ? dir : scl(cp, 1.0 / *depth);
+      *pos = mpr_pos(P);
+      return 1;
+    }
+    expand_portal(P, &v4);
+  }
+}
+
+/* Box-box: separating-axis test over the 15 axes (3 + 3 face normals, 9 edge-edge cross
+ * products; an edge axis wins only if 1.05 x its overlap is below the best face overlap),
+ * then the contact manifold: face axis -> the incident face of the other box clipped against
+ * the reference face's side planes, points below the reference face (at most 4, chosen by
+ * deepest-first farthest-point sampling); edge axis -> one contact at the midpoint of the two
+ * edges' closest points. Normal A -> B, contact point midway between the surfaces.
+ * (MuJoCo's mjc_BoxBox is not available here; this is the standard SAT + clipping
+ * restatement, with up to 4 contacts per pair.) Returns the number of contacts. */
+#define BB_MAXPT 4
+static v3 mcol(m3 R, int i) { return mk(R.m[i], R.m[3 + i], R.m[6 + i]); }
+static int box_box(const shape* A, const shape* B, v3* pos, double* dist, v3* nout) {
+  v3 a[3], b[3];
+  for (int i = 0; i < 3; i++) { a[i] = mcol(A->R, i); b[i] = mcol(B->R, i); }
+  v3 t = sub(B->c, A->c);
+  double best = INFINITY;
+  int bax = -1;
+  v3 bn = mk(0, 0, 0);
+  for (int k = 0; k < 15; k++) {
+    v3 L;
+    if (k < 3) L = a[k];
+    else if (k < 6) L = b[k - 3];
+    else {
+      L = crs(a[(k - 6) / 3], b[(k - 6) % 3]);
+      double ln = nrm(L);
+      if (ln < 1e-6) continue;  /* parallel edges: covered by the face axes */
+      L = scl(L, 1.0 / ln);
+    }
+    double ra = 0, rb = 0;
+    for (int i = 0; i < 3; i++) { ra += A->hs[i] * fabs(dot(a[i], L)); rb += B->hs[i] * fabs(dot(b[i], L)); }
+    double s = dot(t, L);
+    double ov = ra + rb - fabs(s);
+    if (ov < 0.0) return 0;
+    if (k < 6 ? ov < best : 1.05 * ov < best) { best = ov; bax = k; bn = s >= 0.0 ? L : scl(L, -1.0); }
+  }
+  if (bax >= 6) {  /* edge-edge */
+    int i = (bax - 6) / 3, j = (bax - 6) % 3;
+    v3 pa = A->c, pb = B->c;
+    for (int k = 0; k < 3; k++) {
+      if (k != i) pa = add(pa, scl(a[k], (dot(a[k], bn) >= 0.0 ? 1.0 : -1.0) * A->hs[k]));
+      if (k != j) pb = add(pb, scl(b[k], (dot(b[k], bn) >= 0.0 ? -1.0 : 1.0) * B->hs[k]));
+    }
+    v3 c1, c2;
+    seg_seg(sub(pa, scl(a[i], A->hs[i])), add(pa, scl(a[i], A->hs[i])),
+            sub(pb, scl(b[j], B->hs[j])), add(pb, scl(b[j], B->hs[j])), &c1, &c2);
+    pos[0] = scl(add(c1, c2), 0.5);
+    dist[0] = -best;
+    *nout = bn;
+    return 1;
+  }
+  /* face axis: reference box Rf (owner of the axis) with outward face normal nf toward the
+   * incident box In; contacts keep the normal A -> B */
+  const shape *Rf = bax < 3 ? A : B, *In = bax < 3 ? B : A;
+  const v3* ra = bax < 3 ? a : b;
+  const v3* ia = bax < 3 ? b : a;
+  int fi = bax < 3 ? bax : bax - 3;
+  v3 nf = bax < 3 ? bn : scl(bn, -1.0);
+  /* incident face: the In face most anti-parallel to nf */
+  int ij = 0;
+  double bd = -1.0;
+  for (int k = 0; k < 3; k++) {
+    double d = fabs(dot(ia[k], nf));
+    if (d > bd) { bd = d; ij = k; }
+  }
+  double sg = dot(ia[ij], nf) > 0.0 ? -1.0 : 1.0;
+  int u = (ij + 1) % 3, w = (ij + 2) % 3;
+  v3 fc = add(In->c, scl(ia[ij], sg * In->hs[ij]));
+  v3 poly[8], tmp[8];
+  const double su[4] = {1, -1, -1, 1}, sw[4] = {1, 1, -1, -1};
+  int np = 4;
+  for (int k = 0; k < 4; k++)
+    poly[k] = add(fc, add(scl(ia[u], su[k] * In->hs[u]), scl(ia[w], sw[k] * In->hs[w])));
+  /* Sutherland-Hodgman against the 4 side planes of the reference face */
+  for (int e = 0; e < 4; e++) {
+    int ax = (fi + 1 + e / 2) % 3;
+    double side = (e % 2) ? -1.0 : 1.0;
+    v3 pn = scl(ra[ax], side);
+    double off = dot(pn, Rf->c) + Rf->hs[ax];
+    int nq = 0;
+    for (int k = 0; k < np; k++) {
+      v3 p = poly[k], q = poly[(k + 1) % np];
+      double dp = dot(pn, p) - off, dq = dot(pn, q) - off;
+      if (dp <= 0.0) tmp[nq++] = p;
+      if ((dp < 0.0 && dq > 0.0) || (dp > 0.0 && dq < 0.0)) tmp[nq++] = add(p, scl(sub(q, p), dp / (dp - dq)));
+    }
+    np = nq;
+    for (int k = 0; k < np; k++) poly[k] = tmp[k];
+    if (np == 0) return 0;
+  }
+  double fo = dot(nf, Rf->c) + Rf->hs[fi];
+  v3 cp[8];
+  double cd[8];
+  int nc = 0;
+  for (int k = 0; k < np; k++) {
+    double d = fo - dot(nf, poly[k]);
+    if (d >= 0.0) { cp[nc] = poly[k]; cd[nc] = d; nc++; }
+  }
+  int sel[BB_MAXPT], ns = 0;
+  if (nc > 0) {
+    int i0 = 0;
+    for (int k = 1; k < nc; k++) if (cd[k] > cd[i0]) i0 = k;
+    sel[ns++] = i0;
+    while (ns < BB_MAXPT && ns < nc) {
+      int bi = -1;
+      double bdist = -1.0;
+      for (int k = 0; k < nc; k++) {
+        double md = INFINITY;
+        int used = 0;
+        for (int q = 0; q < ns; q++) {
+          if (sel[q] == k) used = 1;
+          md = fmin(md, nrm(sub(cp[k], cp[sel[q]])));
+        }
+        if (!used && md > bdist) { bdist = md; bi = k; }
+      }
+      sel[ns++] = bi;
+    }
+  }
+  for (int q = 0; q < ns; q++) {
+    pos[q] = add(cp[sel[q]], scl(nf, 0.5 * cd[sel[q]]));
+    dist[q] = -cd[sel[q]];
+  }
+  *nout = bn;
+  return ns;
+}
+
+static shape capsule_shape(const envdata* E, int h, int g, const ps_model_desc* d) {
+  shape s;
+  memset(&s, 0, sizeof(s));
+  s.type = 0; s.p0 = E->cap0[h][g]; s.p1 = E->cap1[h][g]; s.r = d->geom_radius[h][g];
+  return s;
+}
+static shape extra_shape(const envdata* E, int h, int i, const ps_model_desc* d) {
+  shape s;
+  memset(&s, 0, sizeof(s));
+  s.type = d->xgeom_type[h][i]; s.c = E->xc[h][i]; s.R = E->xR[h][i];
+  for (int k = 0; k < 3; k++) s.hs[k] = d->xgeom_size[h][i][k];
+  s.vert = (const double(*)[3])d->hull_vert[h][d->xgeom_vert[h][i][0]];
+  s.nvert = d->xgeom_vert[h][i][1];
+  return s;
+}
+static shape box_shape(v3 c, m3 R, const double* hs) {
+  shape s;
+  memset(&s, 0, sizeof(s));
+  s.type = PS_GEOM_BOX; s.c = c; s.R = R;
+  for (int k = 0; k < 3; k++) s.hs[k] = hs[k];
+  return s;
+}
+
+/* narrow phase of box/hull A (geom1) and box/hull/capsule B (geom2), contacts into E with the
+ * normal A -> B; sub = contact index within the pair */
+static void extra_pair(envdata* E, int maxc, contact proto, const shape* A, const shape* B) {
+  if (A->type == PS_GEOM_BOX && B->type == PS_GEOM_BOX) {
+    v3 pos[BB_MAXPT], n;
+    double dist[BB_MAXPT];
+    int k = box_box(A, B, pos, dist, &n);
+    for (int q = 0; q < k; q++) {
+      contact cc = proto;
+      cc.pos = pos[q]; cc.n = n; cc.dist = dist[q]; cc.sub = q;
+      make_frame(n, &cc.t1, &cc.t2);
+      add_contact(E, maxc, &cc);
+    }
+    return;
+  }
+  double depth;
+  v3 n, pos;
+  if (!mpr_penetration(A, B, &depth, &n, &pos)) return;
+  if (nrm(n) == 0.0) n = mk(0, 0, 1);  /* touching: no direction (zero depth) */
+  contact cc = proto;
+  cc.pos = pos; cc.n = n; cc.dist = -depth; cc.sub = 0;
+  make_frame(n, &cc.t1, &cc.t2);
+  add_contact(E, maxc, &cc);
+}
+
 static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
   const ps_model_desc* d = &m->d;
   int maxc = cfg->max_contacts;
@@ -613,6 +983,7 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
   v3 bc = mk(d->base_pos[0], d->base_pos[1], d->base_pos[2]);
   for (int h = 0; h < NH; h++) {
     for (int g = 0; g < NG; g++) {
+      if (d->geom_body[h][g] < 0) continue;  /* unused slot */
       v3 p0 = E->cap0[h][g], p1 = E->cap1[h][g];
       double r = d->geom_radius[h][g];
       double lo[3], hi[3];
@@ -622,7 +993,7 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
       }
       contact proto;
       memset(&proto, 0, sizeof(proto));
-      proto.h2 = h; proto.b2 = d->geom_body[h][g]; proto.g2 = h * NG + g;
+      proto.h2 = h; proto.b2 = d->geom_body[h][g]; proto.g2 = h * NG + g; proto.g1 = -1;
       for (int k = 0; k < NK; k++) {
         /* conservative broadphase: key AABB over its motion */
         if (hi[1] < m->key_y_lo[k] || lo[1] > m->key_y_hi[k]) continue;
@@ -633,6 +1004,29 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
       }
       proto.kind = 1; proto.key = -1;
       capsule_box(E, maxc, proto, p0, p1, r, bc, I3, d->base_half);
+    }
+  }
+  /* extra colliders (box / hull) against the keys and the base, after every capsule */
+  for (int h = 0; h < NH; h++) {
+    for (int i = 0; i < NX; i++) {
+      if (d->xgeom_type[h][i] == PS_GEOM_NONE) continue;
+      shape B = extra_shape(E, h, i, d);
+      double rb = d->xgeom_rbound[h][i], lo[3], hi[3];
+      for (int k = 0; k < 3; k++) { lo[k] = B.c.v[k] - rb; hi[k] = B.c.v[k] + rb; }
+      contact proto;
+      memset(&proto, 0, sizeof(proto));
+      proto.h2 = h; proto.b2 = d->xgeom_body[h][i]; proto.g2 = NCAPS + h * NX + i; proto.g1 = -1;
+      for (int k = 0; k < NK; k++) {
+        if (hi[1] < m->key_y_lo[k] || lo[1] > m->key_y_hi[k]) continue;
+        if (lo[2] > d->key_pos[k][2] + d->key_half[k][2] + 0.02) continue;
+        if (hi[0] < d->key_pos[k][0] - d->key_half[k][0] - 0.02 || lo[0] > d->key_pos[k][0] + d->key_half[k][0] + 0.02) continue;
+        proto.kind = 0; proto.key = k;
+        shape A = box_shape(E->keyc[k], E->keyR[k], d->key_half[k]);
+        extra_pair(E, maxc, proto, &A, &B);
+      }
+      proto.kind = 1; proto.key = -1;
+      shape A = box_shape(bc, I3, d->base_half);
+      extra_pair(E, maxc, proto, &A, &B);
     }
   }
   for (int i = 0; i < d->n_cappairs; i++) {
@@ -659,6 +1053,43 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
     make_frame(cc.n, &cc.t1, &cc.t2);
     add_contact(E, maxc, &cc);  /* past the cap: counted in nfound, not kept */
   }
+  /* hand-hand pairs with an extra collider: bounding spheres, then capsule-box (normal box ->
+   * capsule, the box as geom1), box-box or MPR (normal geom a -> geom b) */
+  for (int i = 0; i < d->n_xpairs; i++) {
+    int ga = d->xpair[i][0], gb = d->xpair[i][1];
+    shape S[2];
+    int hh[2], bb[2];
+    double bound = 0.0;
+    v3 cen[2];
+    for (int q = 0; q < 2; q++) {
+      int g = q ? gb : ga;
+      if (g < NCAPS) {
+        int h = g / NG, l = g % NG;
+        S[q] = capsule_shape(E, h, l, d);
+        hh[q] = h; bb[q] = d->geom_body[h][l];
+        bound += d->geom_halflen[h][l] + d->geom_radius[h][l];
+      } else {
+        int h = (g - NCAPS) / NX, l = (g - NCAPS) % NX;
+        S[q] = extra_shape(E, h, l, d);
+        hh[q] = h; bb[q] = d->xgeom_body[h][l];
+        bound += d->xgeom_rbound[h][l];
+      }
+      cen[q] = shape_centre(&S[q]);
+    }
+    if (nrm(sub(cen[0], cen[1])) > bound) continue;
+    contact proto;
+    memset(&proto, 0, sizeof(proto));
+    proto.kind = 2; proto.key = -1;
+    if (S[0].type == 0 && S[1].type == PS_GEOM_BOX) {
+      proto.h1 = hh[1]; proto.b1 = bb[1]; proto.g1 = gb;
+      proto.h2 = hh[0]; proto.b2 = bb[0]; proto.g2 = ga;
+      capsule_box(E, maxc, proto, S[0].p0, S[0].p1, S[0].r, S[1].c, S[1].R, S[1].hs);
+      continue;
+    }
+    proto.h1 = hh[0]; proto.b1 = bb[0]; proto.g1 = ga;
+    proto.h2 = hh[1]; proto.b2 = bb[1]; proto.g2 = gb;
+    extra_pair(E, maxc, proto, &S[0], &S[1]);
+  }
 }
 
 /* ------------------------------------------------------------------ constraints */
@@ -676,7 +1107,7 @@ static uint32_t row_id_limit(int dof, int side) { return (0u << 30) | ((uint32_t
 static uint32_t row_id_key(int key, int side) { return (1u << 30) | ((uint32_t)key << 1) | (uint32_t)side; }
 static uint32_t row_id_contact(const contact* c, int edge) {
   uint32_t cid = c->kind == 2 ? (uint32_t)(NH * NG * (NK + 1) * 3 + c->g1 * NH * NG + c->g2)
-                              : (uint32_t)((c->g2 * (NK + 1) + (c->key < 0 ? NK : c->key)) * 3 + c->sub);
+                              : (uint32_t)((c->g2 * (NK + 1) + (c->key < 0 ? NK : c->key)) * 4 + c->sub);
   return (2u << 30) | (cid << 2) | (uint32_t)edge;
 }
 
@@ -1282,8 +1713,8 @@ static void control_step(ref_env* R, envdata* E, const float* a, float* obs, flo
     for (int c = 0; c < E->ncon; c++) {
       const contact* cc = &E->con[c];
       if (cc->kind != 2) continue;
-      int la = cc->g1 % NG, lb = cc->g2 % NG;
-      if (cc->g1 / NG != cc->g2 / NG && la < d->root_geom_count && lb < d->root_geom_count) hit = 1;
+      /* has_collision(rh root-body geoms, lh root-body geoms), piano_with_shadow_hands.py:251-259 */
+      if (cc->h1 != cc->h2 && cc->b1 == 0 && cc->b2 == 0) hit = 1;
     }
     fore = hit ? 0.0 : 0.5;
   }
@@ -1521,4 +1952,42 @@ int ref_debug_contacts(ref_env* R, int i, int32_t* info, double* data) {
     for (int k = 0; k < 3; k++) { data[7 * c + 1 + k] = E->con[c].pos.v[k]; data[7 * c + 4 + k] = E->con[c].n.v[k]; }
   }
   return E->ncon;
+}
+
+/* Narrow phase of two world colliders (test access). A shape is packed as 23 doubles: type
+ * (0 capsule, PS_GEOM_BOX, PS_GEOM_HULL), centre (3), row-major rotation (9), capsule p0 (3),
+ * p1 (3), radius, box half sizes (3); hull vertices (geom frame) come separately. A is geom1.
+ * Writes up to 4 contacts as pos (3), normal geom1 -> geom2 (3), dist; returns their number.
+ * A capsule A with a box B is collided as the kernel's hand-hand pairs do: the box becomes
+ * geom1 (the normal then points box -> capsule). */
+static shape unpack_shape(const double* p, const double* verts, int nv) {
+  shape s;
+  memset(&s, 0, sizeof(s));
+  s.type = (int)p[0];
+  s.c = mk(p[1], p[2], p[3]);
+  for (int i = 0; i < 9; i++) s.R.m[i] = p[4 + i];
+  s.p0 = mk(p[13], p[14], p[15]);
+  s.p1 = mk(p[16], p[17], p[18]);
+  s.r = p[19];
+  for (int i = 0; i < 3; i++) s.hs[i] = p[20 + i];
+  s.vert = (const double(*)[3])verts;
+  s.nvert = nv;
+  if (s.type == 0) s.c = scl(add(s.p0, s.p1), 0.5);
+  return s;
+}
+int ref_narrow(const double* pa, const double* va, int nva, const double* pb, const double* vb, int nvb, double* out) {
+  static envdata E;
+  E.ncon = 0;
+  E.nfound = 0;
+  shape A = unpack_shape(pa, va, nva), B = unpack_shape(pb, vb, nvb);
+  contact proto;
+  memset(&proto, 0, sizeof(proto));
+  proto.kind = 2;
+  if (A.type == 0 && B.type == PS_GEOM_BOX) capsule_box(&E, 4, proto, A.p0, A.p1, A.r, B.c, B.R, B.hs);
+  else extra_pair(&E, 4, proto, &A, &B);
+  for (int i = 0; i < E.ncon; i++) {
+    for (int k = 0; k < 3; k++) { out[7 * i + k] = E.con[i].pos.v[k]; out[7 * i + 3 + k] = E.con[i].n.v[k]; }
+    out[7 * i + 6] = E.con[i].dist;
+  }
+  return E.ncon;
 }

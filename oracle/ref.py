@@ -60,6 +60,7 @@ def _bind(L):
     L.ref_set_hand_offset.argtypes = [C.c_void_p, _f64p]
     L.ref_hand_offset_draw.restype = C.c_float
     L.ref_hand_offset_draw.argtypes = [C.c_uint64, C.c_int, C.c_int]
+    L.ref_narrow.argtypes = [_f64p, C.c_void_p, C.c_int, _f64p, C.c_void_p, C.c_int, _f64p]
     _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
     L.ref_stats_get.argtypes = [_i64p] * 5
     L.ref_pdas_hist_get.argtypes = [_i64p]
@@ -234,6 +235,14 @@ class OracleEnv:
         return [(int(info[4 * c]), int(info[4 * c + 1]), int(info[4 * c + 2]), int(info[4 * c + 3]), float(data[7 * c]))
                 for c in range(n)]
 
+    def contacts_full(self, i):
+        """[(kind, key, g1, g2, dist, pos[3], normal[3])] of env i (as BatchedPianoEnv.contacts)."""
+        info = np.zeros(4 * 24, np.int32)
+        data = np.zeros(7 * 24)
+        n = self._L.ref_debug_contacts(self._h, i, info, data)
+        return [(int(info[4 * c]), int(info[4 * c + 1]), int(info[4 * c + 2]), int(info[4 * c + 3]), float(data[7 * c]),
+                 data[7 * c + 1:7 * c + 4].copy(), data[7 * c + 4:7 * c + 7].copy()) for c in range(n)]
+
     def hand_offset(self):
         """(y shift of both hand roots this episode [N], resets so far [N])."""
         dy = np.zeros(self.n)
@@ -251,6 +260,25 @@ class OracleEnv:
 def hand_offset_draw(seed: int, env: int, episode: int) -> float:
     """The randomize_hand_positions draw of (seed, env, episode) (float32, as the GPU's)."""
     return lib().ref_hand_offset_draw(seed, env, episode)
+
+
+def shape(kind, c=(0, 0, 0), R=None, p0=(0, 0, 0), p1=(0, 0, 0), r=0.0, hs=(0, 0, 0), verts=None):
+    """A collider for narrow(): kind "capsule" | "box" | "hull"."""
+    t = {"capsule": 0, "box": 1, "hull": 2}[kind]
+    R = np.eye(3) if R is None else np.asarray(R, np.float64)
+    packed = np.concatenate([[t], c, R.ravel(), p0, p1, [r], hs]).astype(np.float64)
+    v = None if verts is None else np.ascontiguousarray(verts, dtype=np.float64)
+    return packed, v
+
+
+def narrow(a, b):
+    """Contacts of collider a (geom1) with collider b: [(pos, normal geom1 -> geom2, dist)]
+    (capsule a with box b: the box is geom1, the normal points box -> capsule)."""
+    (pa, va), (pb, vb) = a, b
+    out = np.zeros(4 * 7)
+    n = lib().ref_narrow(pa, None if va is None else va.ctypes.data, 0 if va is None else len(va),
+                         pb, None if vb is None else vb.ctypes.data, 0 if vb is None else len(vb), out)
+    return [(out[7 * i:7 * i + 3].copy(), out[7 * i + 3:7 * i + 6].copy(), float(out[7 * i + 6])) for i in range(n)]
 
 
 def prf(y_true, y_pred):

@@ -106,7 +106,7 @@ def test_cylinder_collider_becomes_capsule_and_visuals_are_skipped(mj, base_xml)
     assert spec.geoms[0].radius == 0.035 and spec.geoms[0].halflen == 0.06
     xml = _edit(base_xml, '<geom class="plastic_visual" mesh="forearm" />',
                 '<geom class="plastic_visual" mesh="forearm" contype="1" />')
-    with pytest.raises(ValueError, match="collider type 'mesh'"):
+    with pytest.raises(ValueError, match="unknown mesh 'forearm'"):  # a colliding mesh needs its asset
         mj.load_hand(xml)
 
 
@@ -125,9 +125,16 @@ def test_fullinertia_matches_diaginertia(dp, mj, base_xml):
 def test_errors(mj, base_xml):
     with pytest.raises(ValueError, match="not an MJCF"):
         mj.load_hand("<robot/>")
-    with pytest.raises(ValueError, match="capsule colliders"):
+    extra = '<geom class="plastic_collision" size="0.01 0.01" />' * 9  # 20 + 9 capsules
+    with pytest.raises(ValueError, match="capsule/cylinder colliders"):
         mj.load_hand(_edit(base_xml, '<geom class="plastic_collision" size="0.035 0.06" pos="0.0 0.0 0.11" '
-                                     'quat="1.0 0.0 0.0 0.0" />', ""))
+                                     'quat="1.0 0.0 0.0 0.0" />',
+                           '<geom class="plastic_collision" size="0.035 0.06" pos="0.0 0.0 0.11" '
+                           'quat="1.0 0.0 0.0 0.0" />' + extra))
+    with pytest.raises(ValueError, match="collider type 'sphere'"):
+        mj.load_hand(_edit(base_xml, '<geom class="plastic_collision" size="0.035 0.06" pos="0.0 0.0 0.11" '
+                                     'quat="1.0 0.0 0.0 0.0" />',
+                           '<geom class="plastic_collision" type="sphere" size="0.035" />'))
     with pytest.raises(ValueError, match="unknown default class"):
         mj.load_hand(_edit(base_xml, 'class="wrist"', 'class="nope"'))
     with pytest.raises(ValueError, match="stiffness"):

@@ -17,7 +17,9 @@ from helpers import song  # noqa: E402
 def throughput(name, n, steps=20):
     import os
     solver = os.environ.get("PIANOSIM_SOLVER", "exact")  # "pgs": the round-1 solver (A/B against old builds)
-    task = dp.TaskConfig(trim_silence=name != "twinkle", constraint_solver=solver)
+    warm = os.environ.get("PIANOSIM_WARMUP")  # warm-up PGS sweeps of the exact solve (default 8)
+    task = dp.TaskConfig(trim_silence=name != "twinkle", constraint_solver=solver,
+                         pgs_iterations=None if warm is None else int(warm))
     g = dp.BatchedPianoEnv(n, song(dp, name), task, device="cuda:0")
     g.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(12345)
@@ -35,7 +37,7 @@ def throughput(name, n, steps=20):
     r = sorted(rates)[2]
     lib = Path(dp._lib.LIB_PATH).name
     print(f"{name:15s} N={n:6d}: {r:12,.0f} env-steps/s ({n / r * 1e3:.3f} ms/step) "
-          f"[min {min(rates):,.0f} max {max(rates):,.0f}] {lib} solver={solver}", flush=True)
+          f"[min {min(rates):,.0f} max {max(rates):,.0f}] {lib} solver={solver} warmup={task.pgs_iterations}", flush=True)
 
 
 if __name__ == "__main__":
