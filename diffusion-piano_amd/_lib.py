@@ -22,7 +22,18 @@ EXPORTS = (
 # Every entry point declared in include/pianorl.h.
 RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample",
               "prl_clip_adam", "prl_gather_minibatch", "prl_lnrelu_fwd", "prl_lnrelu_bwd", "prl_actor_head",
-              "prl_critic_head", "prl_colsums")
+              "prl_critic_head", "prl_colsums", "prl_mlp_step_work", "prl_mlp_step")
+
+
+class PrlLayer(C.Structure):  # prl_layer of include/pianorl.h
+    _fields_ = [("in_", C.c_int), ("out", C.c_int), ("W", C.c_void_p), ("b", C.c_void_p), ("gamma", C.c_void_p),
+                ("beta", C.c_void_p), ("dropout", C.c_float), ("dW", C.c_void_p), ("db", C.c_void_p),
+                ("dgamma", C.c_void_p), ("dbeta", C.c_void_p)]
+
+
+class PrlNet(C.Structure):  # prl_net
+    _fields_ = [("nlayers", C.c_int), ("head", C.c_int), ("layer", PrlLayer * 4), ("log_std", C.c_void_p),
+                ("dlog_std", C.c_void_p)]
 
 _lib = None
 _rl = None
@@ -100,8 +111,14 @@ def load_rl() -> C.CDLL:
     L.prl_critic_head.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
     L.prl_colsums.argtypes = [i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(f32), C.POINTER(vp), i32, vp, C.c_size_t,
                               vp]
+    if hasattr(L, "prl_mlp_step"):
+        L.prl_mlp_step_work.argtypes = [C.POINTER(PrlNet), i32, i32]
+        L.prl_mlp_step.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, i32, f32, f32, f32, u64, vp, vp, vp,
+                                   C.c_size_t, vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
+    if hasattr(L, "prl_mlp_step_work"):
+        L.prl_mlp_step_work.restype = C.c_size_t
     _rl = L
     return L
 

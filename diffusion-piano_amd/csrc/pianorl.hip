@@ -490,6 +490,8 @@ __global__ void colsums_final_kernel(ColSums cs, int nchunks) {
   cs.dst[i][c] = acc * cs.scale[i];
 }
 
+#include "mlp_step.inc"
+
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI
@@ -646,5 +648,167 @@ int prl_colsums(int n, const float* const* src, const int* cols, const float* sc
   }
   return 0;
 }
+
+// ---------------------------------------------------------------- fused minibatch step on the matrix cores (mlp_step.inc)
+namespace {
+// work layout of prl_mlp_step: the per-tile partial rows [tiles][total] (bias / LayerNorm /
+// log_std column sums and the 6 logged sums), then per network the inputs of layers 1..3
+// [B][in] and every layer's dZ [B][out]; the reduction entries and the weight-gradient tiles
+int mlp_layout(const prl_net* nets, int sdim, int B, float* work, float* log_row, mlp::Args* a, mlp::GradArgs* g,
+               size_t* work_floats) {
+  int off = 0, ne = 0;
+  auto entry = [&](int n, float* dst, float scale) {
+    if (ne >= mlp::MAXRED) return -1;
+    g->e[ne] = mlp::RedEntry{off, n, scale, dst};
+    ne++;
+    const int o = off;
+    off += n;
+    return o;
+  };
+  size_t scratch = 0;  // floats of X / dZ scratch, placed after the partial rows below
+  for (int i = 0; i < 2; i++) {
+    const prl_net& n = nets[i];
+    if (n.nlayers != mlp::MAXL) return fail("prl_mlp_step: networks of 3 hidden layers + an output layer");
+    if (n.head != i) return fail("prl_mlp_step: nets[0] is the actor (head 0), nets[1] the critic (head 1)");
+    mlp::Net& d = a->net[i];
+    d.nl = n.nlayers;
+    d.head = n.head;
+    int in = sdim;
+    for (int l = 0; l < n.nlayers; l++) {
+      const prl_layer& L = n.layer[l];
+      const bool hidden = l + 1 < n.nlayers;
+      if (L.in != in) return fail("prl_mlp_step: layer widths do not chain");
+      if (hidden && (L.out <= 0 || L.out > mlp::HMAX || L.out % 16))
+        return fail("prl_mlp_step: hidden widths must be multiples of 16 up to 256");
+      if (!hidden && (L.out <= 0 || L.out > 64)) return fail("prl_mlp_step: output width must be 1..64");
+      if (!L.W || !L.b || !L.dW || !L.db || (hidden && (!L.gamma || !L.beta || !L.dgamma || !L.dbeta)))
+        return fail("prl_mlp_step: null layer pointer");
+      mlp::Layer& o = d.L[l];
+      o.in = L.in;
+      o.out = L.out;
+      o.W = L.W;
+      o.b = L.b;
+      o.g = L.gamma;
+      o.be = L.beta;
+      o.p = hidden ? L.dropout : 0.f;
+      o.dW = L.dW;
+      o.ob = entry(L.out, L.db, 1.f);
+      o.og = hidden ? entry(L.out, L.dgamma, 1.f) : 0;
+      o.obe = hidden ? entry(L.out, L.dbeta, 1.f) : 0;
+      // scratch offsets for now; made pointers once the partial block's size is known
+      o.X = l ? reinterpret_cast<float*>(scratch) : nullptr;
+      scratch += l ? (size_t)B * L.in : 0;
+      o.dZ = reinterpret_cast<float*>(scratch);
+      scratch += (size_t)B * L.out;
+      in = L.out;
+    }
+    d.log_std = n.log_std;
+    d.ols = 0;
+    if (i == 0) {
+      if (!n.log_std || !n.dlog_std) return fail("prl_mlp_step: the actor needs log_std and its gradient");
+      d.ols = entry(n.layer[n.nlayers - 1].out, n.dlog_std, 1.f);
+    } else if (n.layer[n.nlayers - 1].out != 1) {
+      return fail("prl_mlp_step: the critic's output width must be 1");
+    }
+  }
+  a->ostat = entry(6, log_row, 1.f / (float)B);
+  if (a->ostat < 0) return fail("prl_mlp_step: too many gradient entries");
+  a->total = off;
+  const int ntiles = (B + mlp::MT - 1) / mlp::MT;
+  const size_t npart = (size_t)ntiles * off;
+  *work_floats = npart + scratch;
+  if (!work) return 0;  // size query
+  // pointers: partial rows, then the scratch
+  g->ne = ne;
+  g->total = off;
+  g->ntiles = ntiles;
+  g->part = work;
+  g->rfirst[0] = 0;
+  for (int e = 0; e < ne; e++) g->rfirst[e + 1] = g->rfirst[e] + (g->e[e].n + 63) / 64;
+  int gl = 0, tiles = 0;
+  for (int i = 0; i < 2; i++)
+    for (int l = 0; l < mlp::MAXL; l++) {
+      mlp::Layer& o = a->net[i].L[l];
+      o.X = l ? work + npart + reinterpret_cast<size_t>(o.X) : nullptr;
+      o.dZ = work + npart + reinterpret_cast<size_t>(o.dZ);
+      g->X[gl] = o.X;  // layer 0: the state rows, set by the caller
+      g->dZ[gl] = o.dZ;
+      g->dW[gl] = o.dW;
+      g->N[gl] = o.out;
+      g->K[gl] = o.in;
+      g->tk[gl] = (o.in + 15) / 16;
+      g->first[gl] = tiles;
+      tiles += ((o.out + 15) / 16) * g->tk[gl];
+      gl++;
+    }
+  g->first[gl] = tiles;
+  g->nl = gl;
+  g->ntw = tiles;
+  g->B = B;
+  return 0;
+}
+}  // namespace
+
+size_t prl_mlp_step_work(const prl_net* nets, int sdim, int B) {
+  mlp::Args a{};
+  mlp::GradArgs g{};
+  float dummy;
+  size_t wf = 0;
+  if (!nets || B <= 0 || sdim <= 0 || mlp_layout(nets, sdim, B, nullptr, &dummy, &a, &g, &wf)) return 0;
+  return wf;
+}
+
+int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
+                 const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
+                 const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream) {
+  if (!nets || !S || !A || !old_lp || !adv || !ret || !step || !log_row || !work) return fail("prl_mlp_step: null argument");
+  if (B <= 0 || sdim <= 0 || sdim > 1024) return fail("prl_mlp_step: B > 0 and 0 < sdim <= 1024 required");
+  mlp::Args a{};
+  mlp::GradArgs g{};
+  size_t need = 0;
+  if (mlp_layout(nets, sdim, B, work, log_row, &a, &g, &need)) return -1;
+  if (nets[0].layer[3].out != adim) return fail("prl_mlp_step: actor output width != action dim");
+  if (work_floats < need) return fail("prl_mlp_step: work space too small (prl_mlp_step_work)");
+  const int KS = ((sdim + 15) & ~15) + 4;
+  const size_t lds = mlp::lds_floats(KS) * sizeof(float);
+  if (lds > 160 * 1024) return fail("prl_mlp_step: state too wide for the LDS tile");
+  a.nnets = 2;
+  a.S = S;
+  a.A = A;
+  a.LP = old_lp;
+  a.ADV = adv;
+  a.RET = ret;
+  a.sdim = sdim;
+  a.adim = adim;
+  a.B = B;
+  a.clip = clip;
+  a.ent = ent_coef;
+  a.eps = ln_eps;
+  a.seed = seed;
+  a.step = step;
+  a.part = work;
+  g.X[0] = S;
+  g.X[mlp::MAXL] = S;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void*)mlp::mlp_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(mlp::mlp_rows_kernel, dim3(g.ntiles, 2), dim3(mlp::NT), lds, (hipStream_t)stream, a);
+  HIPCHK(hipGetLastError());
+  const int waves = g.ntw + g.rfirst[g.ne];
+  hipLaunchKernelGGL(mlp::mlp_grad_kernel, dim3((waves + mlp::GWV - 1) / mlp::GWV), dim3(mlp::GWV * 64), 0,
+                     (hipStream_t)stream, g);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+#ifdef MLP_TIMING
+int prl_mlp_timing_get(uint64_t* out /* host [2][32] */) {
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(mlp::g_tstamp), sizeof(uint64_t) * 64));
+  return 0;
+}
+#endif
 
 }  // extern "C"

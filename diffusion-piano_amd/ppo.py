@@ -41,6 +41,7 @@ There is no CPU fallback: the agent needs a ROCm GPU and libpianorl.so.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 import time
 import warnings
@@ -209,18 +210,29 @@ def loader_permutation(n: int) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------- flat parameter state
+FLAT_ALIGN = 16  # floats: every tensor of the flat buffers starts on a 64-byte boundary, so the
+                 # minibatch kernels read weight rows with 16-byte loads (the gaps stay zero)
+
+
+def flat_offsets(params):
+    """Offsets of ``params`` in a flat buffer (each rounded up to FLAT_ALIGN) and its length."""
+    offs, o = [], 0
+    for p in params:
+        offs.append(o)
+        o += -(-p.numel() // FLAT_ALIGN) * FLAT_ALIGN
+    return offs, o
+
+
 class GradBucket:
     """One flat fp32 buffer holding the gradients of ``params`` (``p.grad`` are views), so
     data-parallel training does one all-reduce per minibatch instead of one per tensor."""
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
+        offs, n = flat_offsets(self.params)
         self.flat = torch.zeros(n, dtype=torch.float32, device=self.params[0].device)
-        o = 0
-        for p in self.params:
+        for p, o in zip(self.params, offs):
             p.grad = self.flat[o:o + p.numel()].view_as(p)
-            o += p.numel()
 
     def allreduce_(self, group=None):
         import torch.distributed as dist
@@ -244,17 +256,20 @@ class FlatAdam(GradBucket):
         segs = [[p for g in opt.param_groups for p in g["params"]] for opt in optimizers]
         params = [p for seg in segs for p in seg]
         dev = params[0].device
-        n = sum(p.numel() for p in params)
-        self.param = torch.empty(n, dtype=torch.float32, device=dev)
-        o = 0
-        for p in params:  # parameters become views of the flat buffer
+        offs, n = flat_offsets(params)
+        self.param = torch.zeros(n, dtype=torch.float32, device=dev)
+        for p, o in zip(params, offs):  # parameters become views of the flat buffer
             self.param[o:o + p.numel()].copy_(p.data.reshape(-1))
             p.data = self.param[o:o + p.numel()].view_as(p)
-            o += p.numel()
         super().__init__(params)
         self.exp_avg = torch.zeros_like(self.param)
         self.exp_avg_sq = torch.zeros_like(self.param)
-        self.seg_end = (C.c_int64 * len(segs))(*np.cumsum([sum(p.numel() for p in seg) for seg in segs]).tolist())
+        self._offs = offs
+        ends, k = [], 0
+        for seg in segs:  # a segment ends where the next one's first tensor starts
+            k += len(seg)
+            ends.append(offs[k] if k < len(offs) else n)
+        self.seg_end = (C.c_int64 * len(segs))(*ends)
         self.nseg = len(segs)
         self.lr = torch.tensor([float(x) for x in lrs], dtype=torch.float32, device=dev)
         self.step_count = torch.zeros(self.nseg, dtype=torch.float32, device=dev)
@@ -266,12 +281,12 @@ class FlatAdam(GradBucket):
         self._bind_state()
 
     def _views(self):
-        o = 0
+        offs = iter(self._offs)
         for s, opt in enumerate(self.optimizers):
             for g in opt.param_groups:
                 for p in g["params"]:
+                    o = next(offs)
                     yield s, p, slice(o, o + p.numel())
-                    o += p.numel()
 
     def _bind_state(self):
         for s, p, sl in self._views():
@@ -314,8 +329,15 @@ class FusedStep:
     ~40 launches instead of the ~150 of torch autograd. Numerically the same math as the
     autograd path (tests/test_gpu_ppo.py compares them)."""
 
+    # minibatches up to this many rows run as ONE matrix-core kernel (prl_mlp_step: every layer
+    # of both networks in LDS, a workgroup per 16 rows) + one gradient reduction; larger ones
+    # keep the hipBLASLt GEMMs, which fill the GPU on their own
+    MFMA_MAX_ROWS = 512
+
     def __init__(self, agent: "PPOAgent"):
         self.agent = agent
+        self.mfma = os.environ.get("PIANORL_NO_MFMA") is None
+        self.nets = {}
         a, c = agent.actor.network, agent.critic.network
         # (linear, layernorm, dropout p) per hidden layer, then the output linear
         self.actor = [(a[0], a[2], 0.0), (a[3], a[5], 0.0), (a[6], a[8], 0.0)], a[9]
@@ -367,6 +389,37 @@ class FusedStep:
         with torch.no_grad():  # the backward is written out: no autograd graph
             self._step(idx)
 
+    def _mlp_nets(self, train):
+        """prl_net descriptors of (actor, critic) for prl_mlp_step (cached per dropout mode)."""
+        if train in self.nets:
+            return self.nets[train]
+        nets = (_lib.PrlNet * 2)()
+        for i, (hidden, out) in enumerate((self.actor, self.critic)):
+            nets[i].nlayers, nets[i].head = 4, i
+            for l, (lin, ln, p) in enumerate(hidden):
+                L = nets[i].layer[l]
+                L.in_, L.out = lin.in_features, lin.out_features
+                L.W, L.b, L.gamma, L.beta = (lin.weight.data_ptr(), lin.bias.data_ptr(), ln.weight.data_ptr(),
+                                             ln.bias.data_ptr())
+                L.dropout = float(p) if (i == 0 or train) else 0.0
+                L.dW, L.db, L.dgamma, L.dbeta = (lin.weight.grad.data_ptr(), lin.bias.grad.data_ptr(),
+                                                 ln.weight.grad.data_ptr(), ln.bias.grad.data_ptr())
+            L = nets[i].layer[3]
+            L.in_, L.out = out.in_features, out.out_features
+            L.W, L.b, L.dW, L.db = out.weight.data_ptr(), out.bias.data_ptr(), out.weight.grad.data_ptr(), \
+                out.bias.grad.data_ptr()
+        nets[0].log_std = self.agent.actor.log_std.data_ptr()
+        nets[0].dlog_std = self.agent.actor.log_std.grad.data_ptr()
+        self.nets[train] = nets
+        return nets
+
+    def _mlp_ok(self, B):
+        if not self.mfma or B > self.MFMA_MAX_ROWS:
+            return False
+        hidden_ok = all(lin.out_features % 16 == 0 and lin.out_features <= 256
+                        for lin, _, _ in self.actor[0] + self.critic[0])
+        return hidden_ok and self.actor[1].out_features <= 64 and self.agent._S.shape[1] <= 384
+
     def _step(self, idx):
         ag, R, st = self.agent, _lib.load_rl(), _stream()
         B = idx.numel()
@@ -377,6 +430,17 @@ class FusedStep:
         chk(R.prl_gather_minibatch(ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(), ag._ADV.data_ptr(),
                                    ag._RET.data_ptr(), idx.data_ptr(), B, b["S"].data_ptr(), b["A"].data_ptr(),
                                    b["LP"].data_ptr(), b["ADV"].data_ptr(), b["RET"].data_ptr(), self.step.data_ptr(), st))
+        if self._mlp_ok(B):
+            nets = self._mlp_nets(train)
+            if "_mlp_work" not in b:
+                n = R.prl_mlp_step_work(nets, sdim, B)
+                b["_mlp_work"] = torch.empty(max(int(n), 1), device=ag.device, dtype=torch.float32)
+            w = b["_mlp_work"]
+            chk(R.prl_mlp_step(nets, b["S"].data_ptr(), sdim, b["A"].data_ptr(), adim, b["LP"].data_ptr(),
+                               b["ADV"].data_ptr(), b["RET"].data_ptr(), B, float(ag.epsilon), float(ag.entropy_coef),
+                               float(self.actor[0][0][1].eps), self.seed, self.step.data_ptr(), ag._log_row.data_ptr(),
+                               w.data_ptr(), w.numel(), st))
+            return
         for net, (hidden, out) in (("a", self.actor), ("c", self.critic)):
             x = b["S"]
             for i, (lin, ln, p) in enumerate(hidden):  # forward

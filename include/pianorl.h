@@ -113,6 +113,34 @@ int prl_critic_head(const float* Z, const float* bias, const float* ret, int B, 
 int prl_colsums(int n, const float* const* src, const int* cols, const float* scale, float* const* dst, int B,
                 float* scratch, size_t scratch_floats, void* stream);
 
+/* One PPO minibatch step (ppo_v2.py:266-293: actor and critic forward, clipped surrogate and
+ * MSE heads, the whole backward) on the matrix cores: a workgroup per 16 minibatch rows and
+ * network runs every layer in LDS (v_mfma_f32_16x16x4_f32, exact fp32), then one launch adds
+ * the per-tile gradient partials in tile order (deterministic). Replaces the ~40 launches of
+ * prl_gather_minibatch's followers (GEMMs + lnrelu_fwd/bwd + heads + colsums) for small
+ * minibatches. Network i = layers 0..2 (Linear -> ReLU -> LayerNorm (eps ln_eps) -> Dropout
+ * p) and the output Linear; nets[0] = actor (tanh mean, Gaussian with log_std, head 0),
+ * nets[1] = critic (head 1). Gradients are written (not accumulated) to the d* pointers;
+ * log_row [6] = the means of actor loss rows, critic squared errors, entropy, value, return,
+ * advantage. Dropout masks are prl_lnrelu_fwd's (seed, *step, layer, row, column). All
+ * pointers device; nets is a host array. work: prl_mlp_step_work(nets, sdim, B) floats. */
+typedef struct {
+  int in, out;
+  const float *W, *b, *gamma, *beta;  /* W [out][in]; gamma/beta: NULL on the output layer */
+  float dropout;
+  float *dW, *db, *dgamma, *dbeta;
+} prl_layer;
+typedef struct {
+  int nlayers, head;  /* 4; 0 actor, 1 critic */
+  prl_layer layer[4];
+  const float* log_std;
+  float* dlog_std;
+} prl_net;
+size_t prl_mlp_step_work(const prl_net* nets, int sdim, int B);
+int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
+                 const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
+                 const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
