@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#define PS_PARK_WORDS 57  // sizeof(LaneDyn) / 4 (static_assert in kernel_v2.inc)
 #include "devmodel.h"
 #include "prims.h"
 #include "collide_x.h"
@@ -53,6 +54,7 @@ struct ps_env {
   float* hand_dy;           // randomize_hand_positions: this episode's y shift of both hands
   int* episode;             // resets so far per env (the draw counter)
   int* stats;               // [N][PS_NSTATS] solver / cap counters of the last step
+  float* park;              // [N][PS_PARK_WORDS][64] kernel scratch (lane state around the MFMA solve)
   uint64_t seed;
   bool has_x;               // box / hull colliders: the pianosim_kernel<true> instantiation
   Contact* con_out;         // [N][MAXCON] contact lists of the last step (ps_record_contacts)
@@ -479,6 +481,7 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMalloc(&E->hand_dy, sizeof(float) * N));
   HIPCHK(hipMalloc(&E->episode, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->stats, sizeof(int) * N * PS_NSTATS));
+  HIPCHK(hipMalloc(&E->park, sizeof(float) * N * PS_PARK_WORDS * 64));
   HIPCHK(hipMemset(E->hand_dy, 0, sizeof(float) * N));
   HIPCHK(hipMemset(E->episode, 0, sizeof(int) * N));
   HIPCHK(hipMemset(E->stats, 0, sizeof(int) * N * PS_NSTATS));
@@ -511,7 +514,7 @@ void ps_destroy(ps_env* E) {
   hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
   hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
-  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats);
+  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats); hipFree(E->park);
   if (E->con_out) hipFree(E->con_out);
   delete E;
 }
@@ -523,6 +526,11 @@ void ps_destroy(ps_env* E) {
 // the first wave of workgroups and the cheap ones fill the slots freed late (longest-
 // processing-time-first): the launch's tail is shorter. Each env's result is independent of
 // the order.
+#ifdef PS_DYN_LDS
+#define PS_LAUNCH_LDS PS_DYN_LDS
+#else
+#define PS_LAUNCH_LDS 0
+#endif
 constexpr int ORDER_THREADS = 1024;
 constexpr int ORDER_BUCKETS = 66;  // 0: resets, 1 + min(rows, 64)
 __global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restrict__ stats,
@@ -559,7 +567,7 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
           (uint32_t)E->seed, (uint32_t)(E->seed >> 32)};
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt,
-         E->hand_dy, E->episode, E->stats, E->con_out};
+         E->hand_dy, E->episode, E->stats, E->con_out, E->park};
   const int* order = nullptr;
   if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
     hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->stats, E->last, E->order,
@@ -568,10 +576,10 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
     order = E->order;
   }
   if (E->has_x)
-    hipLaunchKernelGGL(pianosim_kernel<true>, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b,
+    hipLaunchKernelGGL(pianosim_kernel<true>, dim3(E->n), dim3(64), PS_LAUNCH_LDS, (hipStream_t)stream, E->d_model, song, cfg, b,
                        action, mask, obs, reward, discount, step_type, mode, E->n, order);
   else
-    hipLaunchKernelGGL(pianosim_kernel<false>, dim3(E->n), dim3(64), 0, (hipStream_t)stream, E->d_model, song, cfg, b,
+    hipLaunchKernelGGL(pianosim_kernel<false>, dim3(E->n), dim3(64), PS_LAUNCH_LDS, (hipStream_t)stream, E->d_model, song, cfg, b,
                        action, mask, obs, reward, discount, step_type, mode, E->n, order);
   HIPCHK(hipGetLastError());
   return 0;

@@ -16,7 +16,7 @@ if [ $RC -gt 1 ]; then exit 9; fi
 : > gpurun_out/ab.txt
 for i in 1 2; do
   for L in libpianosim_base.so libpianosim.so; do
-    PIANOSIM_LIB=diffusion-piano_amd/$L timeout -k 10 200 python tools/throughput.py crossing_field 4096 16384 >> gpurun_out/ab.txt 2>&1 || exit 6
+    PIANOSIM_LIB=diffusion-piano_amd/$L timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 >> gpurun_out/ab.txt 2>&1 || exit 6
   done
 done
 cat gpurun_out/ab.txt
