@@ -112,3 +112,36 @@ def test_same_key_contacts_bitwise_repeatable(dp, ref):
         q = g.get_state()["qpos"]
         assert torch.equal(q, q[:1].expand_as(q))
         assert torch.equal(obs, obs[:1].expand_as(obs)) and torch.equal(rew, rew[:1].expand_as(rew))
+
+
+def test_exact_solver_large_free_sets(dp, ref):
+    """States whose coupled-row count passes 40 (free sets above 32 rows go to the matrix-core
+    block Cholesky, ldl_mfma) replayed on the oracle: the same step to the tolerance of the
+    64-env bench-song test above, on the heaviest states the workload produces."""
+    N = 2048
+    md, g, _ = _pair(dp, ref, "crossing_field", N)
+    lo, hi = dp_action_spec(md)
+    rng = np.random.RandomState(7)
+    g.reset()
+    states, acts, outs = [], [], []
+    for _ in range(14):
+        s0 = {k: v.cpu().numpy() for k, v in g.get_state().items()}
+        a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
+        g.step(torch.from_numpy(a).cuda())
+        heavy = np.nonzero((g.solver_stats().cpu().numpy()[:, 3] > 40) & (s0["last"] == 0))[0]
+        if len(heavy):
+            q1 = g.get_state()["qpos"].cpu().numpy()
+            states.append({k: s0[k][heavy] for k in KEYS})
+            acts.append(a[heavy])
+            outs.append(q1[heavy])
+    n = sum(len(x) for x in acts)
+    assert n >= 4, f"only {n} heavy env-steps"
+    st = {k: np.concatenate([s[k] for s in states]) for k in KEYS}
+    seq = song(dp, "crossing_field")
+    _, sttab, tc = dp.compile_task(seq, dp.TaskConfig(trim_silence=True), canonical_actions=False)
+    o = ref.OracleEnv(md, sttab, tc, n)
+    o.set_state(st)
+    o.step(np.concatenate(acts))
+    e = np.abs(np.concatenate(outs) - o.get_state()["qpos"]).max(axis=1)
+    print(f"{n} heavy env-steps: qpos err median {np.median(e):.2e} p90 {np.percentile(e, 90):.2e} max {e.max():.2e}")
+    assert np.median(e) < 1e-5 and np.percentile(e, 90) < 1e-4, (np.median(e), np.percentile(e, 90), e.max())
