@@ -1215,6 +1215,7 @@ static double delassus(const envdata* E, const row* a, const row* b) {
   return s;
 }
 
+#define REF_BIG_SWEEPS 2  /* kernel_v2.inc PS_BIG_SWEEPS */
 #define BPP_MAXIT 32
 #define BPP_TOL 1e-10  /* infeasibility below this fraction of max|f| (f) or max|b| (w) is rounding */
 /* Exact solve of the coupled rows' dual problem
@@ -1427,7 +1428,11 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     r->f = 0.0;
     for (int k = 0; k < NV; k++) w[k] += r->y[k] * r->f;
   }
+  /* the exact solve's warm-up: cfg->pgs_iterations sweeps, at most REF_BIG_SWEEPS above 32
+   * coupled rows (the kernel factors those free sets on the matrix cores, where a solve costs
+   * about five sweeps) */
   int maxit = ref_pgs_mode == 1 ? ref_pgs_maxit : cfg->pgs_iterations, it;
+  if (ref_pgs_mode == 0 && cfg->solver == PS_SOLVER_EXACT && ncoup > 32 && maxit > REF_BIG_SWEEPS) maxit = REF_BIG_SWEEPS;
   for (it = 0; it < maxit; it++) {
     double dfmax = 0.0, fmaxabs = 0.0;
     for (int i = 0; i < nr; i++) {
