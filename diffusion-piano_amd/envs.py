@@ -100,7 +100,7 @@ class TaskConfig:
     # converge to), after `pgs_iterations` warm-up sweeps; "pgs" = `pgs_iterations` cold-start
     # projected Gauss-Seidel sweeps only (truncated, the round-1 solver).
     constraint_solver: str = "exact"
-    pgs_iterations: Optional[int] = None  # None: 8 warm-up sweeps (exact) / 20 sweeps (pgs)
+    pgs_iterations: Optional[int] = None  # None: 2 warm-up sweeps (exact) / 20 sweeps (pgs)
     max_contacts: int = 20
     hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
 
@@ -144,7 +144,7 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
         raise ValueError(f"constraint_solver must be 'exact' or 'pgs', got {cfg.constraint_solver!r}")
     tc.solver = abi.SOLVER_EXACT if cfg.constraint_solver == "exact" else abi.SOLVER_PGS
     tc.pgs_iterations = cfg.pgs_iterations if cfg.pgs_iterations is not None else (
-        8 if cfg.constraint_solver == "exact" else 20)
+        2 if cfg.constraint_solver == "exact" else 20)  # (exact: BPP exchanges are single pivots)
     tc.randomize_hand_positions = int(cfg.randomize_hand_positions)
     tc.max_contacts = min(cfg.max_contacts, abi.MAX_CONTACTS_LIMIT)
     tc.canonical_actions = int(canonical_actions)
