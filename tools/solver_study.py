@@ -125,7 +125,7 @@ def main():
     p.add_argument("--envs", type=int, default=64)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--every", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=8)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--songs", default="crossing_field,twinkle,guren")
     args = p.parse_args()
     dp = importlib.import_module("diffusion-piano_amd")
