@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#define PS_PARK_WORDS 57  // sizeof(LaneDyn) / 4 (static_assert in kernel_v2.inc)
+#define PS_PARK_WORDS 34  // LaneDyn words live across the solve (static_assert in kernel_v2.inc)
 #include "devmodel.h"
 #include "prims.h"
 #include "collide_x.h"
@@ -54,7 +54,7 @@ struct ps_env {
   float* hand_dy;           // randomize_hand_positions: this episode's y shift of both hands
   int* episode;             // resets so far per env (the draw counter)
   int* stats;               // [N][PS_NSTATS] solver / cap counters of the last step
-  float* park;              // [N][PS_PARK_WORDS][64] kernel scratch (lane state around the MFMA solve)
+  float* park;              // [N][PS_PARK_WORDS][64] kernel scratch (lane state around the tableau solve)
   uint64_t seed;
   bool has_x;               // box / hull colliders: the pianosim_kernel<true> instantiation
   Contact* con_out;         // [N][MAXCON] contact lists of the last step (ps_record_contacts)
