@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#define PS_PARK_WORDS 34  // LaneDyn words live across the solve (static_assert in kernel_v2.inc)
+#define PS_PARK_WORDS 43  // LaneDyn words live across the solve (static_assert in kernel_v2.inc)
 #include "devmodel.h"
 #include "prims.h"
 #include "collide_x.h"
