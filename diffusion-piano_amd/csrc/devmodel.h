@@ -74,6 +74,8 @@ struct DevModel {
   float act_c0[NU], act_c1[NU], act_kp[NU], act_clo[NU], act_chi[NU], act_flo[NU], act_fhi[NU];
   // colliders: the body of every collider (capsules, then extras); capsule geometry
   int geom_body[NCOLL];
+  uint64_t geom_pathmask[NCOLL];  // body_pathmask / body_binv of geom_body: one load, not two
+  float geom_binv[NCOLL];
   float geom_pos[NGT][3], geom_axis[NGT][3], geom_hl[NGT], geom_r[NGT];
   int root_geom_count;
   // fingertip sites

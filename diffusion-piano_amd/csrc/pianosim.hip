@@ -317,6 +317,10 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       if (t == PS_GEOM_BOX && !(d->xgeom_size[h][i][0] > 0 && d->xgeom_size[h][i][1] > 0 && d->xgeom_size[h][i][2] > 0))
         return fail("box half sizes must be positive");
     }
+  for (int g = 0; g < NCOLL; g++) {
+    m->geom_pathmask[g] = m->body_pathmask[m->geom_body[g]];
+    m->geom_binv[g] = m->body_binv[m->geom_body[g]];
+  }
   for (int h = 0; h < NH; h++)
     for (int v = 0; v < PS_HAND_HULLVERT; v++) {
       for (int k = 0; k < 3; k++) m->hull_v[h * PS_HAND_HULLVERT + v][k] = (float)d->hull_vert[h][v][k];
