@@ -26,6 +26,9 @@ if [ -f diffusion-piano_amd/libpianosim_timing.so ]; then
   (echo "# tools/phase_timing.py 4096 crossing_field (PIANOSIM_LIB=libpianosim_timing.so, -DPS_TIMING), MI355X, random actions";
    PIANOSIM_LIB=diffusion-piano_amd/libpianosim_timing.so timeout -k 10 120 python tools/phase_timing.py 4096 crossing_field) > profiles/${P}_phase_timing.txt 2>/dev/null || exit 5
 fi
+if [ -f diffusion-piano_amd/libpianosim_timing.so ]; then
+  PIANOSIM_LIB=diffusion-piano_amd/libpianosim_timing.so timeout -k 10 120 python tools/tail_timing.py 1024 twinkle > profiles/${P}_tail_1024.txt 2>/dev/null || exit 5
+fi
 timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 > profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/throughput.py twinkle 1024 4096 >> profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/ppo_bench.py --mode reference --iters 3 --warmup 2 > profiles/${P}_ppo_bench.jsonl 2>/dev/null || exit 8
