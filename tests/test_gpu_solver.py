@@ -115,9 +115,10 @@ def test_same_key_contacts_bitwise_repeatable(dp, ref):
 
 
 def test_exact_solver_large_free_sets(dp, ref):
-    """States whose coupled-row count passes 40 (free sets above 32 rows go to the matrix-core
-    block Cholesky, ldl_mfma) replayed on the oracle: the same step to the tolerance of the
-    64-env bench-song test above, on the heaviest states the workload produces."""
+    """States whose coupled-row count passes 40 (above 32 rows the kernel solves on the
+    48/64-column principal pivot tableau with its lane state parked, dual_ppt) replayed on the
+    oracle: the same step to the tolerance of the 64-env bench-song test above, on the
+    heaviest states the workload produces."""
     N = 2048
     md, g, _ = _pair(dp, ref, "crossing_field", N)
     lo, hi = dp_action_spec(md)
