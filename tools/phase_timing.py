@@ -21,12 +21,12 @@ for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
     stats.append(g.solver_stats().cpu().numpy())
 st = np.stack(stats)  # [10, N, 4]
-out = np.zeros((N, 24), np.uint64)
+out = np.zeros((N, 28), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
-names = {0: "kinematics", 1: "dynamics", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
+names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
          3: "factor", 4: "solve_smooth",
          12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T", 15: "cons:finish",
-         16: "pgs:build A", 17: "pgs:sweeps", 18: "ex:rest", 19: "ex:start set", 20: "ex:factor+solve", 21: "ex:w+check", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
+         16: "pgs:build A", 17: "pgs:sweeps", 18: "ex:rest", 19: "ex:start set", 23: "ex:tableau", 20: "ex:factor+solve", 21: "ex:w+check", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
 for i, n in names.items():
     v = out[:, i].astype(np.float64)

@@ -21,12 +21,12 @@ gen = torch.Generator(device="cuda:0").manual_seed(1)
 for _ in range(3):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
 L.ps_debug_timing(g._h, None)
-names = {0: "kinematics", 1: "dynamics", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
+names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
          3: "factor", 4: "solve_smooth", 12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T",
          15: "cons:finish", 16: "pgs:build A", 17: "pgs:sweeps", 18: "ex:rest", 19: "ex:start set",
          23: "ex:tableau", 20: "ex:factor+solve", 21: "ex:w+check", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
 idx = list(names)
-out = np.zeros((N, 24), np.uint64)
+out = np.zeros((N, 28), np.uint64)
 means, maxes, worst_rows, mean_rows, ms, piv = [], [], [], [], [], []
 for s in range(STEPS):
     a = torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1
