@@ -410,6 +410,10 @@ __device__ __forceinline__ float hungarian_tol(int n, int mm, const float* c /*[
     p[0] = i;
     int j0 = 0;
     for (int j = 0; j <= mm; j++) { minv[j] = INFINITY; used[j] = 0; }
+    // every trip marks one more column used, so a finite cost matrix ends this in <= mm + 1
+    // trips; the cap (and j1 = 0 when no column qualifies) only stops non-finite costs from
+    // looping forever
+    int trips = 0;
     do {
       used[j0] = 1;
       int i0 = p[j0], j1 = 0;
@@ -425,8 +429,9 @@ __device__ __forceinline__ float hungarian_tol(int n, int mm, const float* c /*[
         if (used[j]) { u[p[j]] += delta; v[j] -= delta; }
         else minv[j] -= delta;
       j0 = j1;
-    } while (p[j0] != 0);
-    do { int j1 = way[j0]; p[j0] = p[j1]; j0 = j1; } while (j0);
+    } while (p[j0] != 0 && ++trips <= mm);
+    trips = 0;
+    do { int j1 = way[j0]; p[j0] = p[j1]; j0 = j1; } while (j0 && ++trips <= mm);
   }
   float s = 0.f;
   for (int j = 1; j <= mm; j++)

@@ -189,3 +189,25 @@ def test_vectorized_env_outputs_survive_the_next_step(dp):
         assert torch.equal(o0[k], keep0[k]) and torch.equal(o1[k], keep1[k])
     assert torch.equal(r1, r1c)
     assert not torch.equal(o1["piano/state"], o2["piano/state"]) or not torch.equal(r1, r2)
+
+
+def test_non_finite_actions_do_not_stall_the_launch(dp):
+    """A policy that emits NaN / inf actions poisons only its own envs: the launch completes
+    (the OT assignment is bounded against non-finite costs - an unbounded Hungarian search on
+    lane 0 would never return) and every other env steps exactly as it does without them."""
+    N = 64
+    task = dp.TaskConfig(trim_silence=True)  # Crossing Field: ot_fingering reward (Hungarian)
+    a = torch.rand(4, N, 45, device="cuda:0", generator=torch.Generator(device="cuda:0").manual_seed(9)) * 2 - 1
+    bad = a.clone()
+    bad[:, :4] = float("nan")
+    bad[:, 4:6] = float("inf")
+    outs = []
+    for acts in (a, bad):
+        g = dp.BatchedPianoEnv(N, song(dp, "crossing_field"), task, device="cuda:0")
+        g.reset()
+        for t in range(4):
+            obs, rew, disc, st = g.step(acts[t])
+        torch.cuda.synchronize()
+        outs.append((g.get_state()["qpos"].cpu().numpy(), obs.cpu().numpy(), rew.cpu().numpy()))
+    (q0, o0, r0), (q1, o1, r1) = outs
+    assert np.array_equal(q0[6:], q1[6:]) and np.array_equal(o0[6:], o1[6:]) and np.array_equal(r0[6:], r1[6:])
