@@ -189,8 +189,10 @@ typedef struct {
 } ps_task_cfg;
 
 /* Constraint solvers. EXACT: the solution of the coupled rows' dual problem (block principal
- * pivoting over LDL' solves after pgs_iterations warm-up sweeps) = what MuJoCo's solvers
- * converge to. PGS: pgs_iterations cold-start projected Gauss-Seidel sweeps, truncated. */
+ * pivoting after pgs_iterations warm-up sweeps; in the kernel each exchanged row is one
+ * principal pivot of the rows' LCP tableau, in the oracle each iterate an LDL' solve) = what
+ * MuJoCo's solvers converge to. PGS: pgs_iterations cold-start projected Gauss-Seidel sweeps,
+ * truncated. */
 #define PS_SOLVER_PGS 0
 #define PS_SOLVER_EXACT 1
 #define PS_HAND_POSITION_OFFSET 0.05  /* piano_with_shadow_hands.py:46 _POSITION_OFFSET */
