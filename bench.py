@@ -116,7 +116,10 @@ def lib_sha(path=None) -> str:
     quotes a profile measured on the very binary it runs."""
     import hashlib
 
-    p = Path(path) if path else ROOT / "diffusion-piano_amd" / "libpianosim.so"
+    if path is None:  # the library the loader actually binds (PIANOSIM_LIB can point elsewhere)
+        sys.path.insert(0, str(ROOT))
+        path = importlib.import_module("diffusion-piano_amd._lib").LIB_PATH
+    p = Path(path)
     try:
         return hashlib.sha256(p.read_bytes()).hexdigest()[:16]
     except OSError:
@@ -263,7 +266,8 @@ def main():
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
     seq, task = load_song(dp, args.song)
     shard = sharding.shard_envs(args.envs * world, rank, world)  # weak scaling: envs per GPU fixed
-    env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=shard.start)
+    env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
+                             env_offset=shard.start)
     N = shard.count
     gen = torch.Generator(device=dev).manual_seed(12345 + rank)
     pool = max(1, min(args.steps + args.warmup, 64))
@@ -275,6 +279,9 @@ def main():
     # logging only: RCCL all-gather of the episode returns over xGMI, after the timed region
     fin_sum, fin_n, run_sum, n_all = returns.gather()
     mean_ret = run_sum / n_all
+    # per-env float32 returns of each env's last finished episode, all ranks
+    per_env = sharding.gather_episode_returns(returns, shard, args.envs * world)
+    per_env_done = per_env[~torch.isnan(per_env)]
     stats = env.solver_stats().cpu().numpy()
     total_steps = args.envs * world * args.steps
     value = total_steps / elapsed
@@ -298,15 +305,19 @@ def main():
             "data": "synthetic: uniform random canonical actions (torch Philox, seed 12345+rank); episodes "
                     "staggered (env g starts at t_idx = g mod T) so every step auto-resets ~N/T envs",
             "config": {"workload": f"{N} envs/GPU {args.song} random-action rollout, 10 physics substeps "
-                                   f"per env-step, exact constraint solve ({env.task_cfg.pgs_iterations} PGS warm-up sweeps "
-                                   f"+ block principal pivoting)",
+                                   f"per env-step, constraint forces by the primal Newton solve (friction loss, "
+                                   f"uncapped rows)",
                        "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
                        "mean_return_logged": mean_ret, "episodes_finished": fin_n,
+                       "per_env_returns_gathered": int(per_env.numel()),
+                       "mean_last_episode_return": float(per_env_done.mean()) if per_env_done.numel() else None,
                        "lib_sha": sha,
-                       "solver_last_step": {"solves_per_substep": float(stats[:, 0].mean() / 10.0),
+                       "solver_last_step": {"newton_iterations_per_substep": float(stats[:, 0].mean() / 10.0),
                                             "contact_cap_substeps": int(stats[:, 1].sum()),
-                                            "row_cap_substeps": int(stats[:, 2].sum()),
-                                            "max_rows": int(stats[:, 3].max())}},
+                                            "newton_cap_substeps": int(stats[:, 2].sum()),
+                                            "max_contact_rows": int(stats[:, 3].max()),
+                                            "coupled_substep_frac": float(stats[:, 4].sum() / (10.0 * stats.shape[0])),
+                                            "bad_pivot_substeps": int(stats[:, 5].sum())}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,

@@ -16,7 +16,7 @@ EXPORTS = (
     "ps_last_error", "ps_version", "ps_obs_dim", "ps_model_desc_size", "ps_create", "ps_destroy",
     "ps_reset", "ps_step", "ps_get_state", "ps_set_state", "ps_set_applied", "ps_reward_terms",
     "ps_fingertips", "ps_contact_count", "ps_musical_metrics", "ps_solver_stats", "ps_get_hand_offset",
-    "ps_set_hand_offset", "ps_record_contacts", "ps_contacts",
+    "ps_set_hand_offset", "ps_record_contacts", "ps_contacts", "ps_set_env_offset", "ps_warnings",
 )
 
 # Every entry point declared in include/pianorl.h.
@@ -69,8 +69,10 @@ def load() -> C.CDLL:
     L.ps_musical_metrics.argtypes = [vp, vp, vp, vp]
     if hasattr(L, "ps_record_contacts"):
         L.ps_record_contacts.argtypes = [vp, i32]
+    if hasattr(L, "ps_set_env_offset"):
+        L.ps_set_env_offset.argtypes = [vp, C.c_int64]
     for name, argc in (("ps_solver_stats", 3), ("ps_get_hand_offset", 4), ("ps_set_hand_offset", 3),
-                       ("ps_contacts", 3)):
+                       ("ps_contacts", 3), ("ps_warnings", 3)):
         if hasattr(L, name):  # (absent from older builds loaded for A/B runs via PIANOSIM_LIB)
             getattr(L, name).argtypes = [vp] * argc
     for name in EXPORTS:

@@ -21,9 +21,12 @@ MAX_XPAIRS = 1024
 GEOM_NONE, GEOM_BOX, GEOM_HULL = 0, 1, 2
 MAX_NOTES = 16
 MAX_CONTACTS_LIMIT = 24
-MAX_ROWS = 64
 NTERMS = 5
-NSTATS = 4  # ps_solver_stats slots: solves, contact-cap substeps, row-cap substeps, max rows requested
+NSTATS = 6  # ps_solver_stats slots (PS_STAT_*): Newton iterations, contact-cap substeps, iteration-cap
+            # substeps, most rows in a substep, hand-coupled substeps, non-positive pivots
+STAT_SOLVES, STAT_CONTACT_CAP, STAT_ITER_CAP, STAT_MAX_ROWS, STAT_COUPLED, STAT_BAD_PIVOT = range(6)
+NWARN = 3  # ps_warnings slots: mj_checkPos / mj_checkVel / mj_checkAcc resets
+WARN_BADQPOS, WARN_BADQVEL, WARN_BADQACC = range(3)
 NMUSIC = 6  # ps_musical_metrics slots: precision, recall, f1, sustain_precision, sustain_recall, sustain_f1
 FIRST, MID, LAST = 0, 1, 2
 
@@ -79,6 +82,8 @@ class ModelDesc(C.Structure):
         ("xgeom_size", _arr(d, NHAND, HAND_NXGEOM, 3)), ("xgeom_rbound", _arr(d, NHAND, HAND_NXGEOM)),
         ("xgeom_vert", _arr(i32, NHAND, HAND_NXGEOM, 2)), ("hull_vert", _arr(d, NHAND, HAND_HULLVERT, 3)),
         ("n_xpairs", i32), ("xpair", _arr(i32, MAX_XPAIRS, 2)),
+        ("dof_frictionloss", _arr(d, NHAND, HAND_NDOF)), ("friction_solref", _arr(d, 2)),
+        ("friction_solimp", _arr(d, 5)),
     ]
 
 
@@ -107,11 +112,11 @@ class SongDesc(C.Structure):
 class TaskCfg(C.Structure):
     _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
                 ("wrong_press_termination", i32), ("energy_penalty_coef", d),
-                ("pgs_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32),
+                ("solver_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32),
                 ("solver", i32), ("randomize_hand_positions", i32)]
 
 
-SOLVER_PGS, SOLVER_EXACT = 0, 1
+SOLVER_EXACT = SOLVER_NEWTON = 1
 HAND_POSITION_OFFSET = 0.05  # piano_with_shadow_hands.py:46
 
 

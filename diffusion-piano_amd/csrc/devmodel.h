@@ -28,10 +28,9 @@ constexpr int MAXDEP = 9;      // ancestor list length (self + up to 8 ancestors
 constexpr int MAXLEV = 8;      // body tree levels
 constexpr int MAXCHILD = 5;
 constexpr int MAXCON = 24;     // per-env contact capacity of the GPU workspace
-constexpr int MAXROW = PS_MAX_ROWS;
 constexpr int KEYLANE = 52;    // lane that carries a row's key-dof entry
-// Constraint rows y = L^-T J^T are stored compressed: a row touches the ancestor chains of
-// at most two hand bodies (<= 2 * MAXDEP hand dofs, in r_mask bit order) plus one key.
+// Contact direction rows J are stored compressed: a contact touches the ancestor chains of at
+// most two hand bodies (<= 2 * MAXDEP hand dofs, in support-mask bit order) plus one key.
 constexpr int YS = 20;         // row stride: 18 hand slots, [YKEY] = key entry, 1 pad
 constexpr int YKEY = 19;
 constexpr int NTRI = MAXDEP * (MAXDEP - 1) / 2;  // (a,b) pairs 1<=a<=b<=8
@@ -50,6 +49,7 @@ struct DevModel {
   float pc_solref[2], pc_solimp[5], pc_fric;
   float hc_solref[2], hc_solimp[5], hc_fric;
   float lim_solref[2], lim_solimp[5];
+  float fr_solref[2], fr_solimp[5];   // solreffriction / solimpfriction (friction-loss rows)
   // hand bodies, global index B = h*NB + b
   int body_parent[NBT];
   float body_pos[NBT][3], body_Q[NBT][9], body_mass[NBT], body_ipos[NBT][3], body_I[NBT][6];
@@ -61,6 +61,7 @@ struct DevModel {
   // hand dofs, global index g = h*ND + j
   int dof_body[NDT], dof_type[NDT], dof_limited[NDT];
   float dof_axis[NDT][3], dof_lo[NDT], dof_hi[NDT], dof_damp[NDT], dof_arm[NDT], dof_dinv[NDT];
+  float dof_floss[NDT];      // frictionloss (0: no friction-loss row)
   int dof_depth[NDT], dof_anc[NDT][MAXDEP];
   uint64_t dof_ancmask[NDT];
   uint64_t dof_descmask[NDT];  // bit g: hand dof g is a proper descendant

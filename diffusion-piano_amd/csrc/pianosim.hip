@@ -15,7 +15,6 @@
 #include <string>
 #include <vector>
 
-#define PS_PARK_WORDS 43  // LaneDyn words live across the solve (static_assert in kernel_v2.inc)
 #include "devmodel.h"
 #include "prims.h"
 #include "collide_x.h"
@@ -38,6 +37,8 @@ static int fail(const std::string& s) {
 
 struct ps_env {
   int n, device, obs_dim;
+  int64_t env_offset;       // global id of local env 0 (Philox key of the per-env draws)
+  int full_cpl;             // PIANOSIM_DEBUG_FULL_COUPLED: every coupled solve on the 28-column C block
   ps_task_cfg cfg;
   DevModel* d_model;
   int T;
@@ -54,11 +55,30 @@ struct ps_env {
   float* hand_dy;           // randomize_hand_positions: this episode's y shift of both hands
   int* episode;             // resets so far per env (the draw counter)
   int* stats;               // [N][PS_NSTATS] solver / cap counters of the last step
-  float* park;              // [N][PS_PARK_WORDS][64] kernel scratch (lane state around the tableau solve)
+  int* warnings;            // [N][PS_NWARN] physics warnings since create
   uint64_t seed;
   bool has_x;               // box / hull colliders: the pianosim_kernel<true> instantiation
   Contact* con_out;         // [N][MAXCON] contact lists of the last step (ps_record_contacts)
 };
+
+// Every entry point that touches device memory or launches binds the handle's device for its
+// duration and restores the caller's afterwards: two handles on two GPUs in one process, or a
+// null/default stream, never reach the wrong device ("handles are independent", pianosim.h).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+#define GUARD(E)                                                                  \
+  DeviceGuard guard_((E)->device);                                                \
+  if (!guard_.ok) return fail("hipSetDevice(" + std::to_string((E)->device) + ") failed")
 
 static void quat2mat_h(const double* q, float* R) {
   double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
@@ -110,6 +130,8 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     m->lim_solimp[i] = (float)d->limit_solimp[i];
   }
   m->pc_fric = (float)d->piano_contact.friction;
+  for (int i = 0; i < 2; i++) m->fr_solref[i] = (float)d->friction_solref[i];
+  for (int i = 0; i < 5; i++) m->fr_solimp[i] = (float)d->friction_solimp[i];
   m->hc_fric = (float)d->hand_contact.friction;
   // bodies
   int depth_b[NBT];
@@ -161,6 +183,8 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       m->dof_damp[g] = (float)d->dof_damping[h][j];
       m->dof_arm[g] = (float)d->dof_armature[h][j];
       m->dof_dinv[g] = (float)d->dof_invweight[h][j];
+      if (!(d->dof_frictionloss[h][j] >= 0.0)) return fail("negative dof_frictionloss");
+      m->dof_floss[g] = (float)d->dof_frictionloss[h][j];
       if (m->body_dof[B] < 0) m->body_dof[B] = g;
       else if (m->body_dof[B] + m->body_ndof[B] != g) return fail("dofs of a body must be contiguous");
       m->body_ndof[B]++;
@@ -419,7 +443,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
 extern "C" {
 
 const char* ps_last_error(void) { return g_err.c_str(); }
-int ps_version(void) { return 1; }
+int ps_version(void) { return 3; }
 int ps_model_desc_size(void) { return (int)sizeof(ps_model_desc); }
 int ps_obs_dim(const ps_task_cfg* cfg) {
   return (cfg->n_steps_lookahead + 1) * (NK + 1) + (cfg->fingering_reward ? 10 : 0) + NK + 1 + NH * ND;
@@ -432,8 +456,8 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   if (song->T <= 0) return fail("empty song");
   if (cfg->n_steps_lookahead < 0) return fail("negative lookahead");
   if (cfg->max_contacts < 0 || cfg->max_contacts > MAXCON) return fail("max_contacts out of range");
-  if (cfg->pgs_iterations < 0) return fail("negative pgs_iterations");
-  if (cfg->solver != PS_SOLVER_PGS && cfg->solver != PS_SOLVER_EXACT) return fail("unknown solver");
+  if (cfg->solver_iterations < 0) return fail("negative solver_iterations");
+  if (cfg->solver != PS_SOLVER_NEWTON) return fail("unknown solver (PS_SOLVER_NEWTON is the only one)");
   for (int t = 0; t < song->T; t++) {
     if (song->count[t] < 0 || song->count[t] > PS_MAX_NOTES) return fail("bad note count");
     // the ot_fingering reward assigns the step's goal keys to fingertips in a table of
@@ -444,7 +468,8 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
       return fail("step " + std::to_string(t) + " has " + std::to_string(k) + " goal keys; at most " +
                   std::to_string(PS_MAX_NOTES) + " are supported");
   }
-  HIPCHK(hipSetDevice(device));
+  DeviceGuard guard_(device);
+  if (!guard_.ok) return fail("hipSetDevice(" + std::to_string(device) + ") failed");
   DevModel* hm = new DevModel;
   if (build_dev_model(model, hm)) { delete hm; return -1; }
   const bool has_x = hm->nx > 0 || hm->nxpairs > 0;
@@ -485,11 +510,13 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMalloc(&E->hand_dy, sizeof(float) * N));
   HIPCHK(hipMalloc(&E->episode, sizeof(int) * N));
   HIPCHK(hipMalloc(&E->stats, sizeof(int) * N * PS_NSTATS));
-  HIPCHK(hipMalloc(&E->park, sizeof(float) * N * PS_PARK_WORDS * 64));
+  HIPCHK(hipMalloc(&E->warnings, sizeof(int) * N * PS_NWARN));
+  HIPCHK(hipMemset(E->warnings, 0, sizeof(int) * N * PS_NWARN));
   HIPCHK(hipMemset(E->hand_dy, 0, sizeof(float) * N));
   HIPCHK(hipMemset(E->episode, 0, sizeof(int) * N));
   HIPCHK(hipMemset(E->stats, 0, sizeof(int) * N * PS_NSTATS));
   E->seed = seed;
+  E->env_offset = 0;
   HIPCHK(hipMemset(E->qpos, 0, sizeof(float) * N * NV));
   HIPCHK(hipMemset(E->qvel, 0, sizeof(float) * N * NV));
   HIPCHK(hipMemset(E->qws, 0, sizeof(float) * N * NV));
@@ -507,26 +534,26 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipDeviceSynchronize());
   E->applied_on = false;
   E->ordered = !(getenv("PIANOSIM_NO_ORDER") && atoi(getenv("PIANOSIM_NO_ORDER")));
+  E->full_cpl = getenv("PIANOSIM_DEBUG_FULL_COUPLED") && atoi(getenv("PIANOSIM_DEBUG_FULL_COUPLED"));
   *out = E;
   return 0;
 }
 
 void ps_destroy(ps_env* E) {
   if (!E) return;
-  (void)hipSetDevice(E->device);
+  DeviceGuard guard_(E->device);
   hipFree(E->d_model); hipFree(E->d_goal); hipFree(E->d_count); hipFree(E->d_keys); hipFree(E->d_fingers);
   hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
   hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
-  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats); hipFree(E->park);
+  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats); hipFree(E->warnings);
   if (E->con_out) hipFree(E->con_out);
   delete E;
 }
 
 // Dispatch order of a step launch: envs by the cost of their previous step, descending -
-// the most coupled constraint rows one of its substeps requested (PS_STAT_MAX_ROWS: the
-// constraint phases and the exact solve grow with it) - envs about to auto-reset (no physics
-// this step) last. Workgroups are dispatched in blockIdx order, so the expensive envs start in
+// the Newton iterations its substeps took (PS_STAT_SOLVES: each is a Hessian assembly,
+// factorization and line search) - envs about to auto-reset (no physics this step) last. Workgroups are dispatched in blockIdx order, so the expensive envs start in
 // the first wave of workgroups and the cheap ones fill the slots freed late (longest-
 // processing-time-first): the launch's tail is shorter. Each env's result is independent of
 // the order.
@@ -536,7 +563,7 @@ void ps_destroy(ps_env* E) {
 #define PS_LAUNCH_LDS 0
 #endif
 constexpr int ORDER_THREADS = 1024;
-constexpr int ORDER_BUCKETS = 66;  // 0: resets, 1 + min(rows, 64)
+constexpr int ORDER_BUCKETS = 130;  // 0: resets, 1 + min(Newton iterations of the last step, 128)
 __global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restrict__ stats,
                                                               const uint8_t* __restrict__ last,
                                                               int* __restrict__ order, int n) {
@@ -544,7 +571,7 @@ __global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restr
   if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
   __syncthreads();
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int b = last[e] ? 0 : 1 + min(max(stats[(size_t)e * PS_NSTATS + PS_STAT_MAX_ROWS], 0), 64);
+    const int b = last[e] ? 0 : 1 + min(max(stats[(size_t)e * PS_NSTATS + PS_STAT_SOLVES], 0), 128);
     atomicAdd(&hist[b], 1);
   }
   __syncthreads();
@@ -557,7 +584,7 @@ __global__ void __launch_bounds__(ORDER_THREADS) order_kernel(const int* __restr
   }
   __syncthreads();
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int b = last[e] ? 0 : 1 + min(max(stats[(size_t)e * PS_NSTATS + PS_STAT_MAX_ROWS], 0), 64);
+    const int b = last[e] ? 0 : 1 + min(max(stats[(size_t)e * PS_NSTATS + PS_STAT_SOLVES], 0), 128);
     order[atomicAdd(&base[b], 1)] = e;
   }
 }
@@ -566,12 +593,12 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
                   float* discount, uint8_t* step_type, void* stream) {
   Song song{E->T, E->d_goal, E->d_count, E->d_keys, E->d_fingers};
   Cfg cfg{E->cfg.n_steps_lookahead, E->cfg.fingering_reward, E->cfg.forearm_reward, E->cfg.wrong_press_termination,
-          E->cfg.pgs_iterations, E->cfg.max_contacts, E->obs_dim, E->cfg.canonical_actions,
-          (float)E->cfg.energy_penalty_coef, E->cfg.solver == PS_SOLVER_EXACT, E->cfg.randomize_hand_positions != 0,
-          (uint32_t)E->seed, (uint32_t)(E->seed >> 32)};
+          E->cfg.solver_iterations, E->cfg.max_contacts, E->obs_dim, E->cfg.canonical_actions,
+          (float)E->cfg.energy_penalty_coef, E->cfg.randomize_hand_positions != 0,
+          (uint32_t)E->seed, (uint32_t)(E->seed >> 32), (uint32_t)E->env_offset, E->full_cpl};
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt,
-         E->hand_dy, E->episode, E->stats, E->con_out, E->park};
+         E->hand_dy, E->episode, E->stats, E->con_out, E->warnings};
   const int* order = nullptr;
   if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
     hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->stats, E->last, E->order,
@@ -591,18 +618,21 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
 
 int ps_reset(ps_env* E, const uint8_t* env_mask, float* obs, void* stream) {
   if (!E || !obs) return fail("null argument");
+  GUARD(E);
   return launch(E, 1, nullptr, env_mask, obs, nullptr, nullptr, nullptr, stream);
 }
 
 int ps_step(ps_env* E, const float* action, float* obs, float* reward, float* discount, uint8_t* step_type,
             void* stream) {
   if (!E || !action || !obs || !reward || !discount || !step_type) return fail("null argument");
+  GUARD(E);
   return launch(E, 0, action, nullptr, obs, reward, discount, step_type, stream);
 }
 
 int ps_get_state(ps_env* E, float* qpos, float* qvel, float* qacc_ws, float* ctrl, float* sustain, int32_t* t_idx,
                  uint8_t* last, void* stream) {
   if (!E) return fail("null env");
+  GUARD(E);
   hipStream_t s = (hipStream_t)stream;
   size_t N = E->n;
   if (qpos) HIPCHK(hipMemcpyAsync(qpos, E->qpos, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
@@ -618,6 +648,7 @@ int ps_get_state(ps_env* E, float* qpos, float* qvel, float* qacc_ws, float* ctr
 int ps_set_state(ps_env* E, const float* qpos, const float* qvel, const float* qacc_ws, const float* ctrl,
                  const float* sustain, const int32_t* t_idx, const uint8_t* last, void* stream) {
   if (!E) return fail("null env");
+  GUARD(E);
   hipStream_t s = (hipStream_t)stream;
   size_t N = E->n;
   if (qpos) HIPCHK(hipMemcpyAsync(E->qpos, qpos, sizeof(float) * N * NV, hipMemcpyDeviceToDevice, s));
@@ -632,6 +663,7 @@ int ps_set_state(ps_env* E, const float* qpos, const float* qvel, const float* q
 
 int ps_set_applied(ps_env* E, const float* qfrc_applied, void* stream) {
   if (!E) return fail("null env");
+  GUARD(E);
   if (!qfrc_applied) {
     E->applied_on = false;
     return 0;
@@ -644,6 +676,7 @@ int ps_set_applied(ps_env* E, const float* qfrc_applied, void* stream) {
 
 int ps_reward_terms(ps_env* E, float* terms, void* stream) {
   if (!E || !terms) return fail("null argument");
+  GUARD(E);
   HIPCHK(hipMemcpyAsync(terms, E->terms, sizeof(float) * E->n * PS_NTERMS, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream));
   return 0;
@@ -651,6 +684,7 @@ int ps_reward_terms(ps_env* E, float* terms, void* stream) {
 
 int ps_fingertips(ps_env* E, float* xpos, void* stream) {
   if (!E || !xpos) return fail("null argument");
+  GUARD(E);
   HIPCHK(hipMemcpyAsync(xpos, E->tips, sizeof(float) * E->n * 2 * PS_NFINGER * 3, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream));
   return 0;
@@ -679,6 +713,7 @@ int ps_debug_timing(ps_env* E, uint64_t* out) {
 
 int ps_musical_metrics(ps_env* E, float* episode, int32_t* episodes, void* stream) {
   if (!E) return fail("null argument");
+  GUARD(E);
   if (episode)
     HIPCHK(hipMemcpyAsync(episode, E->mus_ep, sizeof(float) * E->n * PS_NMUSIC, hipMemcpyDeviceToDevice,
                           (hipStream_t)stream));
@@ -689,12 +724,14 @@ int ps_musical_metrics(ps_env* E, float* episode, int32_t* episodes, void* strea
 
 int ps_solver_stats(ps_env* E, int32_t* stats, void* stream) {
   if (!E || !stats) return fail("null argument");
+  GUARD(E);
   HIPCHK(hipMemcpyAsync(stats, E->stats, sizeof(int) * E->n * PS_NSTATS, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }
 
 int ps_get_hand_offset(ps_env* E, float* dy, int32_t* episodes, void* stream) {
   if (!E) return fail("null argument");
+  GUARD(E);
   if (dy) HIPCHK(hipMemcpyAsync(dy, E->hand_dy, sizeof(float) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   if (episodes)
     HIPCHK(hipMemcpyAsync(episodes, E->episode, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
@@ -703,6 +740,7 @@ int ps_get_hand_offset(ps_env* E, float* dy, int32_t* episodes, void* stream) {
 
 int ps_set_hand_offset(ps_env* E, const float* dy, void* stream) {
   if (!E || !dy) return fail("null argument");
+  GUARD(E);
   if (!E->cfg.randomize_hand_positions) return fail("ps_set_hand_offset needs randomize_hand_positions");
   HIPCHK(hipMemcpyAsync(E->hand_dy, dy, sizeof(float) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
@@ -711,8 +749,8 @@ int ps_set_hand_offset(ps_env* E, const float* dy, void* stream) {
 static_assert(sizeof(ps_contact) == sizeof(Contact), "ps_contact mirrors the kernel's contact record");
 int ps_record_contacts(ps_env* E, int on) {
   if (!E) return fail("null argument");
+  GUARD(E);
   if (on && !E->con_out) {
-    HIPCHK(hipSetDevice(E->device));
     HIPCHK(hipMalloc(&E->con_out, sizeof(Contact) * MAXCON * (size_t)E->n));
     HIPCHK(hipMemset(E->con_out, 0, sizeof(Contact) * MAXCON * (size_t)E->n));
   } else if (!on && E->con_out) {
@@ -724,14 +762,31 @@ int ps_record_contacts(ps_env* E, int on) {
 
 int ps_contacts(ps_env* E, ps_contact* out, void* stream) {
   if (!E || !out) return fail("null argument");
+  GUARD(E);
   if (!E->con_out) return fail("contact recording is off (ps_record_contacts)");
   HIPCHK(hipMemcpyAsync(out, E->con_out, sizeof(Contact) * MAXCON * (size_t)E->n, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream));
   return 0;
 }
 
+int ps_warnings(ps_env* E, int32_t* warnings, void* stream) {
+  if (!E || !warnings) return fail("null argument");
+  GUARD(E);
+  HIPCHK(hipMemcpyAsync(warnings, E->warnings, sizeof(int) * E->n * PS_NWARN, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream));
+  return 0;
+}
+
+int ps_set_env_offset(ps_env* E, int64_t global_first_env) {
+  if (!E) return fail("null argument");
+  if (global_first_env < 0) return fail("negative env offset");
+  E->env_offset = global_first_env;
+  return 0;
+}
+
 int ps_contact_count(ps_env* E, int32_t* ncon, void* stream) {
   if (!E || !ncon) return fail("null argument");
+  GUARD(E);
   HIPCHK(hipMemcpyAsync(ncon, E->ncon, sizeof(int) * E->n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return 0;
 }

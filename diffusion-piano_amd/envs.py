@@ -96,11 +96,12 @@ class TaskConfig:
     randomize_hand_positions: bool = False  # piano_with_shadow_hands.py:64,491-499
     control_timestep: float = model_lib.CONTROL_TIMESTEP
     physics_timestep: float = model_lib.PHYSICS_TIMESTEP
-    # Constraint solve: "exact" = the solution of the dual problem (what MuJoCo's solvers
-    # converge to), after `pgs_iterations` warm-up sweeps; "pgs" = `pgs_iterations` cold-start
-    # projected Gauss-Seidel sweeps only (truncated, the round-1 solver).
-    constraint_solver: str = "exact"
-    pgs_iterations: Optional[int] = None  # None: 2 warm-up sweeps (exact) / 20 sweeps (pgs)
+    # Constraint solve: "newton" (alias "exact") = MuJoCo's primal problem minimised by Newton
+    # iterations with exact line search (mj_solNewton), to convergence - the unique solution
+    # every MuJoCo solver converges to. `solver_iterations` caps the Newton iterations per
+    # substep (None: the library default, 16). The round-1 truncated "pgs" is retired.
+    constraint_solver: str = "newton"
+    solver_iterations: Optional[int] = None
     max_contacts: int = 20
     hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
 
@@ -140,11 +141,11 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
     tc.forearm_reward = int(not cfg.disable_forearm_reward)
     tc.wrong_press_termination = int(cfg.wrong_press_termination)
     tc.energy_penalty_coef = cfg.energy_penalty_coef
-    if cfg.constraint_solver not in ("exact", "pgs"):
-        raise ValueError(f"constraint_solver must be 'exact' or 'pgs', got {cfg.constraint_solver!r}")
-    tc.solver = abi.SOLVER_EXACT if cfg.constraint_solver == "exact" else abi.SOLVER_PGS
-    tc.pgs_iterations = cfg.pgs_iterations if cfg.pgs_iterations is not None else (
-        2 if cfg.constraint_solver == "exact" else 20)  # (exact: BPP exchanges are single pivots)
+    if cfg.constraint_solver not in ("newton", "exact"):
+        raise ValueError(f"constraint_solver must be 'newton' (or its alias 'exact'), got {cfg.constraint_solver!r}"
+                         " (the round-1 truncated 'pgs' solver is retired)")
+    tc.solver = abi.SOLVER_NEWTON
+    tc.solver_iterations = 0 if cfg.solver_iterations is None else int(cfg.solver_iterations)
     tc.randomize_hand_positions = int(cfg.randomize_hand_positions)
     tc.max_contacts = min(cfg.max_contacts, abi.MAX_CONTACTS_LIMIT)
     tc.canonical_actions = int(canonical_actions)
@@ -171,7 +172,10 @@ class BatchedPianoEnv:
     """N envs on one GPU; all tensors live in HBM (torch-ROCm)."""
 
     def __init__(self, num_envs: int, midi, task: Optional[TaskConfig] = None, device=None,
-                 canonical_actions: bool = True, seed: int = 0):
+                 canonical_actions: bool = True, seed: int = 0, env_offset: int = 0):
+        """``seed`` keys the per-env random draws (randomize_hand_positions); ``env_offset`` is the
+        global id of env 0 when one job's envs are sharded over GPUs (sharding.EnvShard.start), so
+        global env g draws the same values at any world size."""
         import torch
 
         self._torch = torch
@@ -194,6 +198,8 @@ class BatchedPianoEnv:
         _lib.check(L.ps_create(C.addressof(self.model_desc), C.addressof(sd), C.addressof(self.task_cfg),
                                self.num_envs, dev_index, seed, C.byref(h)))
         self._h = h
+        if env_offset:
+            _lib.check(L.ps_set_env_offset(h, int(env_offset)))
         N = self.num_envs
         f32 = dict(device=self.device, dtype=torch.float32)
         self.obs = torch.zeros(N, self.obs_dim, **f32)

@@ -213,6 +213,88 @@ def _strip(name: Optional[str], prefix: str) -> Optional[str]:
     return name
 
 
+# ------------------------------------------------------------------ fail-closed attribute checks
+# The loader must not simulate a different hand than the XML describes: every attribute of the
+# elements it reads is either modelled (read into the HandSpec), irrelevant to the dynamics
+# (names, visuals, solver effort), or held to the single value the kernel simulates - anything
+# else raises ValueError naming the element and attribute.
+MJ_SOLREF = (0.02, 1.0)                   # MuJoCo defaults (mjModel solref / solimp / friction)
+MJ_SOLIMP = (0.9, 0.95, 0.001, 0.5, 2.0)
+MJ_FRICTION = 1.0
+
+_VISUAL = {"name", "class", "group", "rgba", "material", "user"}
+_FRAME = {"pos", "quat", "euler", "axisangle", "zaxis", "xyaxes"}
+_ALLOWED = {
+    "body": _VISUAL | _FRAME | {"childclass"},
+    "inertial": _FRAME | {"mass", "diaginertia", "fullinertia"},
+    "joint": _VISUAL | {"type", "axis", "range", "limited", "damping", "armature", "frictionloss", "springref"},
+    "geom": _VISUAL | _FRAME | {"type", "size", "fromto", "mesh", "contype", "conaffinity", "friction", "solref",
+                                "solimp", "density", "mass", "shellinertia", "fluidshape", "fluidcoef"},
+    "position": _VISUAL | {"joint", "tendon", "kp", "ctrlrange", "ctrllimited", "forcerange", "forcelimited"},
+    "fixed": _VISUAL | {"limited", "solreflimit", "solimplimit", "range"},
+    "option": {"timestep", "iterations", "ls_iterations", "tolerance", "ls_tolerance", "solver", "jacobian",
+               "noslip_tolerance", "ccd_iterations", "ccd_tolerance", "sdf_iterations", "sdf_initpoints",
+               "apirate"},
+    "compiler": {"angle", "autolimits", "eulerseq", "meshdir", "assetdir", "texturedir", "discardvisual",
+                 "strippath", "usethread", "inertiagrouprange", "exactmeshinertia", "saveinertial"},
+}
+# attribute -> (the one value the kernel simulates, parser)
+_NUM = lambda v: tuple(float(x) for x in v.split())
+_FIXED = {
+    "body": {"mocap": ("false", str), "gravcomp": ((0.0,), _NUM)},
+    "joint": {"pos": ((0.0, 0.0, 0.0), _NUM), "ref": ((0.0,), _NUM), "stiffness": ((0.0,), _NUM),
+              "margin": ((0.0,), _NUM), "solreflimit": (MJ_SOLREF, _NUM), "solimplimit": (MJ_SOLIMP, _NUM),
+              "solreffriction": (MJ_SOLREF, _NUM), "solimpfriction": (MJ_SOLIMP, _NUM),
+              "actuatorfrclimited": ("false", str), "actuatorgravcomp": ("false", str)},
+    "geom": {"condim": ((3.0,), _NUM), "margin": ((0.0,), _NUM), "gap": ((0.0,), _NUM),
+             "priority": ((0.0,), _NUM), "solmix": ((1.0,), _NUM)},
+    "position": {"kv": ((0.0,), _NUM), "gear": ((1.0,), _NUM), "dampratio": ((0.0,), _NUM),
+                 "timeconst": ((0.0,), _NUM), "inheritrange": ((0.0,), _NUM), "actlimited": ("false", str),
+                 "actearly": ("false", str)},
+    "fixed": {"stiffness": ((0.0,), _NUM), "damping": ((0.0,), _NUM), "frictionloss": ((0.0,), _NUM),
+              "margin": ((0.0,), _NUM), "springlength": ((-1.0, -1.0), _NUM)},
+    "option": {"integrator": ("Euler", str), "cone": ("pyramidal", str), "impratio": ((1.0,), _NUM),
+               "noslip_iterations": ((0.0,), _NUM), "gravity": ((0.0, 0.0, -9.81), _NUM),
+               "wind": ((0.0, 0.0, 0.0), _NUM), "density": ((0.0,), _NUM), "viscosity": ((0.0,), _NUM),
+               "o_margin": ((0.0,), _NUM)},
+    "compiler": {"inertiafromgeom": ("false|auto", str), "balanceinertia": ("false", str),
+                 "boundmass": ((0.0,), _NUM), "boundinertia": ((0.0,), _NUM), "settotalmass": ((-1.0,), _NUM),
+                 "fusestatic": ("false", str), "coordinate": ("local", str), "alignfree": ("false", str)},
+}
+
+
+def _pad(vals, full):
+    """MuJoCo fills a partial solref / solimp / friction from its defaults."""
+    return tuple(vals) + tuple(full[len(vals):])
+
+
+def check_attrs(kind: str, what: str, a: Dict[str, str]) -> None:
+    """Raise ValueError if ``a`` (an element's attributes with its class defaults merged) holds an
+    attribute the kernel does not simulate, or a held attribute at another value."""
+    allowed, fixed = _ALLOWED[kind], _FIXED.get(kind, {})
+    for k, v in a.items():
+        if k in allowed:
+            continue
+        if k not in fixed:
+            raise ValueError(f"{what}: attribute {k}={v!r} is not supported (the kernel does not model it)")
+        want, parse = fixed[k]
+        if parse is str:
+            ok = v in want.split("|")
+        else:
+            try:
+                got = parse(v)
+            except ValueError:
+                raise ValueError(f"{what}: bad {k}={v!r}") from None
+            ok = len(got) <= len(want) and np.allclose(_pad(got, want), want, rtol=0, atol=1e-12)
+        if not ok:
+            raise ValueError(f"{what}: {k}={v!r} is not supported (the kernel simulates {k}={want!r})")
+
+
+_TOP = {"compiler", "option", "size", "default", "asset", "worldbody", "contact", "tendon", "actuator", "sensor",
+        "keyframe", "visual", "statistic", "custom"}
+_BODY_CHILDREN = {"inertial", "joint", "geom", "body", "site", "camera", "light"}
+
+
 # ------------------------------------------------------------------ loader
 def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     """Read a right-hand MJCF (a path, or the XML text itself) into a ``model.HandSpec``,
@@ -222,6 +304,24 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     root = ET.fromstring(text)
     if root.tag != "mujoco":
         raise ValueError("not an MJCF document (root element is not <mujoco>)")
+    for el in root:
+        if el.tag not in _TOP:
+            raise ValueError(f"<{el.tag}> is not supported (the kernel does not model it)")
+    for opt in root.findall("option"):
+        check_attrs("option", "<option>", dict(opt.attrib))
+        for fl in opt:
+            raise ValueError(f"<option><{fl.tag} {' '.join(f'{k}={v!r}' for k, v in fl.attrib.items())}> "
+                             "is not supported (the kernel runs MuJoCo's default flags)")
+    for comp_el in root.findall("compiler"):
+        check_attrs("compiler", "<compiler>", dict(comp_el.attrib))
+    for cel in root.findall("contact"):
+        for el in cel:
+            if el.tag != "exclude":
+                raise ValueError(f"<contact><{el.tag}> is not supported (only <exclude>)")
+    for tel in root.findall("tendon"):
+        for el in tel:
+            if el.tag != "fixed":
+                raise ValueError(f"<tendon><{el.tag}> is not supported (only two-joint <fixed>)")
     ctx = _Ctx(root)
     base_dir = Path(source).parent if not (isinstance(source, str) and source.lstrip().startswith("<")) else Path(".")
     comp = root.find("compiler")
@@ -256,12 +356,17 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     body_idx: Dict[str, int] = {}
     joint_idx: Dict[str, int] = {}
     root_joint_attrs: Dict[str, str] = {}
+    contact_params = set()
 
     def visit(el: ET.Element, parent: int, cls: str):
         cls = el.get("childclass", cls)
         a = ctx.attrs(el, "body", cls)
         bi = len(bodies)
         name = _strip(a.get("name", f"body{bi}"), prefix)
+        check_attrs("body", f"body {name!r}", {k: v for k, v in el.attrib.items()})
+        for child in el:
+            if child.tag not in _BODY_CHILDREN:
+                raise ValueError(f"body {name!r}: <{child.tag}> is not supported")
         body_idx[name] = bi
         pos = tuple(_floats(a.get("pos", "0 0 0")))
         quat = ctx.frame_quat(a)
@@ -269,6 +374,7 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
         inertial = el.find("inertial")
         if inertial is not None:
             ia = ctx.attrs(inertial, "inertial", cls)
+            check_attrs("inertial", f"body {name!r} <inertial>", ia)
             mass = float(ia["mass"])
             ipos = tuple(_floats(ia.get("pos", "0 0 0")))
             if "diaginertia" in ia:
@@ -287,6 +393,9 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
         bodies.append(M.Body(name, parent, pos, quat, mass, ipos, iquat, diag))
         for j in el.findall("joint"):
             ja = ctx.attrs(j, "joint", cls)
+            if float(ja.get("stiffness", "0")) != 0.0:
+                raise ValueError(f"joint {ja.get('name')!r}: joint stiffness is not supported")
+            check_attrs("joint", f"joint {ja.get('name')!r}", ja)
             if bi == 0:
                 root_joint_attrs.update(ja)
             jtype = ja.get("type", "hinge")
@@ -304,11 +413,23 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
             jname = _strip(ja.get("name", f"joint{len(dofs)}"), prefix)
             joint_idx[jname] = len(dofs)
             dofs.append(M.Dof(jname, bi, kind, tuple(_floats(ja.get("axis", "0 0 1"))), rng,
-                              float(ja.get("damping", "0")), float(ja.get("armature", "0"))))
+                              float(ja.get("damping", "0")), float(ja.get("armature", "0")),
+                              float(ja.get("frictionloss", "0"))))
         for g in el.findall("geom"):
             ga = ctx.attrs(g, "geom", cls)
             if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
                 continue  # visual only
+            check_attrs("geom", f"body {name!r} collider", ga)
+            for bit in ("contype", "conaffinity"):
+                if ga.get(bit, "1") not in ("0", "1"):
+                    raise ValueError(f"body {name!r} collider: {bit}={ga[bit]!r} is not supported (bitmask "
+                                     "filtering is not modelled: 0 or 1)")
+            if ga.get("contype", "1") != "1" or ga.get("conaffinity", "1") != "1":
+                raise ValueError(f"body {name!r} collider: contype/conaffinity other than 1/1 is not supported")
+            param = (_pad(_floats(ga.get("solref", "")) or (), MJ_SOLREF),
+                     _pad(_floats(ga.get("solimp", "")) or (), MJ_SOLIMP),
+                     (_floats(ga.get("friction", "")) or [MJ_FRICTION])[0])
+            contact_params.add(param)
             gtype = ga.get("type", "sphere")
             if gtype not in ("capsule", "cylinder", "box", "mesh"):
                 raise ValueError(f"body {name!r}: collider type {gtype!r} is not supported "
@@ -354,10 +475,11 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
 
     # forearm DOFs on the root body after its own joints (shadow_hand.py:272-311); they
     # take the root's joint defaults (armature), damping is set by build_model (critical)
-    arm = float(ctx.attrs(roots[0].find("joint") if roots[0].find("joint") is not None else ET.Element("joint"),
-                          "joint", roots[0].get("childclass", "main")).get("armature", "0"))
+    ra = ctx.attrs(roots[0].find("joint") if roots[0].find("joint") is not None else ET.Element("joint"),
+                   "joint", roots[0].get("childclass", "main"))
+    arm, floss = float(ra.get("armature", "0")), float(ra.get("frictionloss", "0"))
     n_root = sum(1 for d in dofs if d.body == 0)
-    slides = [M.Dof(n, 0, k, ax, rng, 0.0, arm) for (n, k, ax, rng) in FOREARM_DOFS]
+    slides = [M.Dof(n, 0, k, ax, rng, 0.0, arm, floss) for (n, k, ax, rng) in FOREARM_DOFS]
     dofs[n_root:n_root] = slides
     remap = [i if i < n_root else i + len(slides) for i in range(n_menagerie_joints)]
     joint_idx = {k: remap[v] for k, v in joint_idx.items()}
@@ -367,6 +489,9 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
     tendon_idx: Dict[str, int] = {}
     tel = root.find("tendon")
     for t in ([] if tel is None else tel.findall("fixed")):
+        check_attrs("fixed", f"fixed tendon {t.get('name')!r}", ctx.attrs(t, "fixed", "main"))
+        if t.get("limited", "auto") == "true" or (t.get("limited", "auto") == "auto" and "range" in t.attrib):
+            raise ValueError(f"fixed tendon {t.get('name')!r}: tendon limits are not supported")
         js = t.findall("joint")
         if len(js) != 2:
             raise ValueError(f"fixed tendon {t.get('name')!r}: exactly two joints are supported")
@@ -384,6 +509,7 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
         if a.tag != "position":
             raise ValueError(f"actuator <{a.tag}> is not supported (position only)")
         aa = ctx.attrs(a, "position", "main")
+        check_attrs("position", f"actuator {aa.get('name')!r}", aa)
         if "joint" in aa:
             kind, target = 0, joint_idx.get(_strip(aa["joint"], prefix))
         elif "tendon" in aa:
@@ -425,7 +551,12 @@ def load_hand(source: Union[str, Path], prefix: str = "rh_") -> M.HandSpec:
                             ("box/mesh colliders", len(xgeoms), abi.HAND_NXGEOM)):
         if got > most:
             raise ValueError(f"hand has {got} {what}; the kernel ABI holds at most {most}")
-    return M.HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order, tcoef, xgeoms or None)
+    if len(contact_params) > 1:
+        raise ValueError(f"hand colliders carry {len(contact_params)} different solref/solimp/friction sets; the "
+                         "kernel's hand contact parameters are one set (ps_model_desc.hand_contact)")
+    contact = next(iter(contact_params)) if contact_params else (MJ_SOLREF, MJ_SOLIMP, MJ_FRICTION)
+    return M.HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order, tcoef, xgeoms or None,
+                      contact)
 
 
 # ------------------------------------------------------------------ writer
@@ -442,12 +573,15 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
     ET.SubElement(root, "compiler", angle="radian", autolimits="true")
     dflt = ET.SubElement(root, "default")
     hand = ET.SubElement(dflt, "default", {"class": "right_hand"})
-    ET.SubElement(hand, "joint", axis="1 0 0", damping="0.05", armature=repr(spec.dofs[2].armature))
+    floss = spec.dofs[2].frictionloss
+    ET.SubElement(hand, "joint", axis="1 0 0", damping="0.05", armature=repr(spec.dofs[2].armature),
+                  frictionloss=repr(floss))
     ET.SubElement(hand, "position", forcerange="-1 1")
     wrist = ET.SubElement(hand, "default", {"class": "wrist"})
     ET.SubElement(wrist, "joint", damping="0.5")
+    sr, si, fr = spec.contact or (MJ_SOLREF, MJ_SOLIMP, MJ_FRICTION)
     ET.SubElement(ET.SubElement(hand, "default", {"class": "plastic_collision"}), "geom", type="capsule",
-                  group="3")
+                  group="3", solref=_fmt(sr), solimp=_fmt(si), friction=_fmt((fr, 0.005, 0.0001)))
     ET.SubElement(ET.SubElement(hand, "default", {"class": "plastic_visual"}), "geom", type="mesh",
                   contype="0", conaffinity="0", group="2")
 
@@ -485,6 +619,8 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
                 ja["axis"] = _fmt(d.axis)
             if d.armature != spec.dofs[2].armature:
                 ja["armature"] = repr(d.armature)
+            if d.frictionloss != floss:
+                ja["frictionloss"] = repr(d.frictionloss)
             ET.SubElement(el, "joint", ja)
         ET.SubElement(el, "geom", {"class": "plastic_visual", "mesh": b.name})
         for g in spec.geoms:

@@ -14,7 +14,8 @@ simulates (robopianist/suite/tasks/base.py:45-197):
   gains, fixed J0 tendons) from the public model, with two documented deviations:
   capsule colliders only (the reference's ``primitive_fingertip_collisions`` option,
   shadow_hand.py:144-152, and the MJX attempt's cylinder->capsule conversion,
-  parallelized_base.py:49-64) and no joint frictionloss. Forearm DOFs, their position
+  parallelized_base.py:49-64). Joint frictionloss 0.01 on every joint (the Menagerie
+  right_hand class; hand_provenance.json). Forearm DOFs, their position
   actuators with critical damping and the forearm_tx range follow shadow_hand.py:41-85,
   272-311 and tasks/base.py:160-194. Left hand = mirror image of the right one through
   the hand's x=0 plane.
@@ -142,6 +143,7 @@ class Dof:
     range: Tuple[float, float]
     damping: float
     armature: float = 2e-4
+    frictionloss: float = 0.0   # MuJoCo joint frictionloss (dof_frictionloss)
 
 
 @dataclass
@@ -186,6 +188,7 @@ class HandSpec(NamedTuple):
     obs_order: List[int]                       # joints_pos observation order (dof indices)
     tendon_coef: Optional[List[Tuple[float, float]]] = None  # None = (1, 1) each
     xgeoms: Optional[List[XGeom]] = None       # box / hull colliders beside the capsules
+    contact: Optional[tuple] = None            # collider (solref, solimp, friction); None = HAND_CONTACT
 
 
 ID = (1.0, 0.0, 0.0, 0.0)
@@ -204,6 +207,11 @@ def _finger(prefix, parent, knuckle_pos):
         Body(prefix + "distal", -1, (0, 0, 0.025), ID, 0.013, (0, 0, 0.0130769), QX90,
              (1.28092e-6, 1.12092e-6, 5.3e-7)),
     ]
+
+
+# Menagerie right_hand collision class: solref / solimp / friction of every hand collider
+HAND_CONTACT = ((0.005, 1.0), (0.5, 0.99, 0.0001, 0.5, 2.0), 1.0)
+MENAGERIE_FRICTIONLOSS = 0.01  # shadow_hand/right_hand.xml <default class="right_hand"><joint frictionloss>
 
 
 def _right_hand_tree():
@@ -270,6 +278,10 @@ def _right_hand_tree():
              Dof("THJ2", idx["thmiddle"], 0, NY, (-0.698132, 0.698132), 0.05),
              Dof("THJ1", idx["thdistal"], 0, X, (-0.261799, 1.5708), 0.05)]
     assert len(dofs) == abi.HAND_NDOF
+    # Menagerie right_hand class: frictionloss on every joint; the forearm slides, added under
+    # the root's childclass by _add_dofs (shadow_hand.py:272-311), inherit it
+    for dof in dofs:
+        dof.frictionloss = MENAGERIE_FRICTIONLOSS
     Z = (0.0, 0.0, 1.0)
     geoms = [Geom(idx["forearm"], (0, 0, 0.11), Z, 0.06, 0.035),
              Geom(idx["wrist"], (0, 0, 0), X, 0.015, 0.0135),
@@ -316,7 +328,7 @@ def _right_hand_tree():
     acts = [(k, dof_idx[t] if k == 0 else t, kp, cr, fr) for (k, t, kp, cr, fr) in acts]
     # joints_pos order: Menagerie joints in document order, forearm joints appended last.
     obs_order = list(range(2, abi.HAND_NDOF)) + [0, 1]
-    return HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order)
+    return HandSpec(bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order, contact=HAND_CONTACT)
 
 
 def authored_hand() -> HandSpec:
@@ -392,11 +404,15 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
     m.piano_contact.friction = 1.0
     m.limit_solref[:] = (0.02, 1.0)
     m.limit_solimp[:] = (0.9, 0.95, 0.001, 0.5, 2.0)
-    m.hand_contact.solref[:] = (0.005, 1.0)
-    m.hand_contact.solimp[:] = (0.5, 0.99, 0.0001, 0.5, 2.0)
-    m.hand_contact.friction = 1.0
-
     spec = hand if hand is not None else _right_hand_tree()
+    sr, si, fr = spec.contact if spec.contact is not None else HAND_CONTACT
+    m.hand_contact.solref[:] = sr
+    m.hand_contact.solimp[:] = si
+    m.hand_contact.friction = fr
+    # solreffriction / solimpfriction: MuJoCo's defaults (the reference sets none)
+    m.friction_solref[:] = (0.02, 1.0)
+    m.friction_solimp[:] = (0.9, 0.95, 0.001, 0.5, 2.0)
+
     bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order = spec[:8]
     tcoef = spec.tendon_coef or [(1.0, 1.0)] * len(tendons)
     forearm_mass = _subtree_mass(bodies, 0)
@@ -433,6 +449,7 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
                 damping = 2.0 * math.sqrt(forearm_mass * FOREARM_KP)
             m.dof_damping[h][j] = damping
             m.dof_armature[h][j] = dof.armature
+            m.dof_frictionloss[h][j] = dof.frictionloss
             m.dof_obs_order[h][j] = obs_order[j]
         for g in range(abi.HAND_NGEOM):
             m.geom_body[h][g] = -1  # unused slot

@@ -45,6 +45,8 @@ class EpisodeReturns:
 
         self._torch = torch
         self.running = torch.zeros(num_envs, device=device, dtype=torch.float64)
+        # per env: the return of its most recently finished episode (NaN before the first one)
+        self.last_return = torch.full((num_envs,), float("nan"), device=device, dtype=torch.float32)
         self.finished_sum = torch.zeros((), device=device, dtype=torch.float64)
         self.finished_count = torch.zeros((), device=device, dtype=torch.int64)
 
@@ -55,6 +57,7 @@ class EpisodeReturns:
         first = step_type == 0
         self.running = torch.where(first, torch.zeros_like(self.running), self.running + reward.to(torch.float64))
         last = step_type == 2
+        self.last_return = torch.where(last, self.running.to(torch.float32), self.last_return)
         self.finished_sum += torch.where(last, self.running, torch.zeros_like(self.running)).sum()
         self.finished_count += last.sum()
 
@@ -73,6 +76,28 @@ class EpisodeReturns:
             local = torch.stack(parts).sum(0)
         s, n, rs, ne = (float(x) for x in local.cpu())
         return s, int(n), rs, int(ne)
+
+
+def gather_episode_returns(returns: EpisodeReturns, shard: EnvShard, total: int, group=None):
+    """All ranks: the per-env float32 returns of each env's last finished episode for the whole
+    job, [total] in global env order (``ncclAllGather(float32
+    episode_return[N/8])`` over xGMI; the reference driver keeps per-env returns,
+    parallelized_base_v2.py:151,172). Shards differ in size by at most one env, so every rank
+    sends a buffer padded to the largest shard and the padding is dropped after the gather."""
+    import torch
+    import torch.distributed as dist
+
+    local = returns.last_return
+    if not (dist.is_available() and dist.is_initialized()):
+        return local.clone()
+    world = dist.get_world_size(group)
+    width = -(-total // world)
+    buf = torch.full((width,), float("nan"), device=local.device, dtype=torch.float32)
+    buf[: local.numel()] = local
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    out = [parts[r][: shard_envs(total, r, world).count] for r in range(world)]
+    return torch.cat(out)
 
 
 def max_over_ranks(value: float, device=None, group=None) -> float:

@@ -160,6 +160,13 @@ typedef struct {
    * MuJoCo's filtering; contacts of these follow the capsule-capsule ones */
   int32_t n_xpairs;
   int32_t xpair[PS_MAX_XPAIRS][2];
+  /* joint friction loss (MuJoCo dof_frictionloss; the Menagerie hand's right_hand class sets
+   * 0.01 on every joint): each dof with frictionloss > 0 adds one friction-loss constraint row
+   * J = e_dof, |f| <= frictionloss, to every substep's constraint solve, with the reference
+   * acceleration -b (J v) and regulariser from solreffriction / solimpfriction (MuJoCo's
+   * defaults (0.02, 1) and (0.9, 0.95, 0.001, 0.5, 2) unless the XML sets them). */
+  double dof_frictionloss[PS_NHAND][PS_HAND_NDOF];
+  double friction_solref[2], friction_solimp[5];
 } ps_model_desc;
 
 /* Song tables: NoteTrajectory in dense form (music.py:SongTables). */
@@ -178,29 +185,38 @@ typedef struct {
   int32_t forearm_reward;           /* 1: add forearm reward term */
   int32_t wrong_press_termination;
   double energy_penalty_coef;       /* 5e-3 */
-  int32_t pgs_iterations;           /* PGS sweeps per substep: the whole solve (PS_SOLVER_PGS) or
-                                       the warm-up of the exact solve (PS_SOLVER_EXACT) */
+  int32_t solver_iterations;        /* Newton iterations per substep at most (0: the default cap, 16);
+                                       reaching it is counted (PS_STAT_ITER_CAP) */
   int32_t max_contacts;             /* per env, <= PS_MAX_CONTACTS_LIMIT */
   int32_t canonical_actions;        /* 1: ps_step actions are in [-1,1] and are rescaled to the
                                        spec as dm_env_wrappers.CanonicalSpecWrapper does */
-  int32_t solver;                   /* PS_SOLVER_EXACT (default) or PS_SOLVER_PGS */
+  int32_t solver;                   /* PS_SOLVER_NEWTON (the only value) */
   int32_t randomize_hand_positions; /* piano_with_shadow_hands.py:64,491-499: each episode shifts
                                        both hands by the same U(-0.05, 0.05) m along y */
 } ps_task_cfg;
 
-/* Constraint solvers. EXACT: the solution of the coupled rows' dual problem (block principal
- * pivoting after pgs_iterations warm-up sweeps; in the kernel each exchanged row is one
- * principal pivot of the rows' LCP tableau, in the oracle each iterate an LDL' solve) = what
- * MuJoCo's solvers converge to. PGS: pgs_iterations cold-start projected Gauss-Seidel sweeps,
- * truncated. */
-#define PS_SOLVER_PGS 0
+/* Constraint solver. NEWTON (= EXACT, the only one): the minimiser of MuJoCo's primal
+ * constraint problem over the accelerations (mj_solNewton: Newton directions from the
+ * Hessian M + sum D J'J of the rows in their quadratic zone, exact line search), to fp32
+ * (kernel) / 1e-13 (oracle) precision - the unique solution every MuJoCo solver converges
+ * to. The round-1 truncated PGS (value 0) is retired; ps_create rejects it. */
 #define PS_SOLVER_EXACT 1
+#define PS_SOLVER_NEWTON 1
 #define PS_HAND_POSITION_OFFSET 0.05  /* piano_with_shadow_hands.py:46 _POSITION_OFFSET */
 
 #define PS_MAX_CONTACTS_LIMIT 24
-/* Coupled constraint rows per env (hand limits, contacted-key limits, 4 per contact);
- * rows beyond this are dropped in order. */
-#define PS_MAX_ROWS 64
+/* Constraint rows are not capped: friction loss (one per hand dof with frictionloss), hand and
+ * key limits, 4 pyramid edges per contact. */
+
+/* Physics warnings (MuJoCo mjWARN_BADQPOS / BADQVEL / BADQACC): mj_checkPos / mj_checkVel at
+ * the start of a substep and mj_checkAcc after its constraint solve find a non-finite value or
+ * one beyond 1e10 in qpos / qvel / qacc; the env's physics is reset as mj_resetData does (qpos
+ * = qpos0, qvel = qacc_warmstart = ctrl = qfrc_applied = 0; after a bad qacc the forward
+ * dynamics is recomputed at the reset state) and the warning is counted (ps_warnings). */
+#define PS_WARN_BADQPOS 0
+#define PS_WARN_BADQVEL 1
+#define PS_WARN_BADQACC 2
+#define PS_NWARN 3
 
 /* step_type values (dm_env.StepType) */
 #define PS_FIRST 0
@@ -225,11 +241,14 @@ typedef struct {
 #define PS_NMUSIC 6
 
 /* Slots of ps_solver_stats: per env, over the substeps of its last step. */
-#define PS_STAT_SOLVES 0        /* linear solves of the exact dual solve (summed) */
+#define PS_STAT_SOLVES 0        /* Newton iterations (Hessian factorizations), summed */
 #define PS_STAT_CONTACT_CAP 1   /* substeps whose narrow phase found >= max_contacts contacts */
-#define PS_STAT_ROW_CAP 2       /* substeps that dropped coupled rows past PS_MAX_ROWS */
-#define PS_STAT_MAX_ROWS 3      /* most coupled rows requested in one substep */
-#define PS_NSTATS 4
+#define PS_STAT_ITER_CAP 2      /* substeps whose Newton solve stopped at its iteration cap */
+#define PS_STAT_MAX_ROWS 3      /* most constraint rows in one substep */
+#define PS_STAT_COUPLED 4       /* substeps whose hands were coupled (hand-hand contact or a key
+                                   touched by both hands): the Woodbury-coupled solve */
+#define PS_STAT_BAD_PIVOT 5     /* substeps with a non-positive Cholesky pivot (clamped) */
+#define PS_NSTATS 6
 
 typedef struct ps_env ps_env;
 
@@ -293,11 +312,22 @@ int ps_musical_metrics(ps_env* env, float* episode, int32_t* episodes, void* str
  * counterpart: the evidence that the contact and row caps do not bind. */
 int ps_solver_stats(ps_env* env, int32_t* stats, void* stream);
 
+/* Physics warnings of each env since ps_create, [N][PS_NWARN] int32 (device): the counts of
+ * mj_checkPos / mj_checkVel / mj_checkAcc resets (see PS_WARN_*). dm_control turns a new
+ * warning into PhysicsError (Physics.check_invalid_state); envs.Environment does the same. */
+int ps_warnings(ps_env* env, int32_t* warnings, void* stream);
+
 /* randomize_hand_positions (piano_with_shadow_hands.py:491-499): each env's current y shift of
  * both hand roots [N] f32 and its resets so far [N] i32 (device; either may be NULL). The set
  * form overrides the shift until the env's next reset (teacher-forced parity). */
 int ps_get_hand_offset(ps_env* env, float* dy, int32_t* episodes, void* stream);
 int ps_set_hand_offset(ps_env* env, const float* dy, void* stream);
+
+/* Global id of this handle's env 0 when the envs of one job are sharded over handles/GPUs
+ * (default 0). Every per-env random draw (the randomize_hand_positions Philox stream) is keyed
+ * by (seed, global env id, episode), so a global env draws the same values at any world size
+ * ("Philox streams are keyed by global env id"). */
+int ps_set_env_offset(ps_env* env, int64_t global_first_env);
 
 #ifdef __cplusplus
 }

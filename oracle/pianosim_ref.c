@@ -41,7 +41,6 @@
 #define NCAPS (NH * NG)  /* global collider ids: capsules [0, NCAPS), extras NCAPS + h * NX + i */
 #define NV PS_NV
 #define MAXCON PS_MAX_CONTACTS_LIMIT
-#define MAXROW (4 * MAXCON + NH * ND * 2 + NK)  /* storage; coupled rows are capped at PS_MAX_ROWS */
 #define MINIMP 0.0001
 #define MAXIMP 0.9999
 #define MINVAL 1e-15
@@ -165,12 +164,10 @@ typedef struct {
   v3 keyc[NK], keyanchor[NK];
   /* dynamics */
   double M[NH][ND][ND], Mh[NH][ND][ND], D[NH][ND], Dh[NH][ND];
+  double Mfull[NH][ND][ND];  /* the hand mass matrices before factorization (the Newton Hessian) */
   double Mk[NK], Mkh[NK];
   double bias[NV], passive[NV], actfrc[NV], act_force[PS_NU];
-  /* exact-solve warm start: the previous substep's coupled rows and their free set */
-  int prev_n;
-  uint32_t prev_id[PS_MAX_ROWS];
-  uint8_t prev_free[PS_MAX_ROWS];
+  int warnings[PS_NWARN];  /* mj_checkPos / Vel / Acc resets since create (ps_warnings) */
   /* collision */
   int ncon, nfound;
   contact con[MAXCON];
@@ -188,6 +185,7 @@ struct ref_env {
   int32_t *count, *keys, *fingers;
   int n;
   uint64_t seed;
+  int64_t env_offset;  /* global id of env 0 */
   envdata* e;
 };
 typedef struct ref_env ref_env;
@@ -1093,23 +1091,17 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
 }
 
 /* ------------------------------------------------------------------ constraints */
+/* Constraint rows of one substep (MuJoCo mj_makeConstraint order: friction loss, limits,
+ * contacts). Every row is J (dense over the dofs, sparse in practice), its reference
+ * acceleration aref, regulariser R (D = 1/R) and type; J x - aref = jar is the row's
+ * constraint-space residual at the acceleration x. */
+enum { ROW_FRICTION = 0, ROW_LIMIT = 1, ROW_CONTACT = 2 };
 typedef struct {
-  double J[NV];   /* dense over all dofs (sparse in practice) */
-  double y[NV];   /* L^-T J^T */
-  double Aii, R, aref, b, f;
-  int closed;     /* free key limit row (solved in closed form) */
-  uint32_t id;    /* identity across substeps (row_id): warm start of the exact solve */
+  double J[NV];
+  double aref, R, D, floss;  /* floss: friction-loss bound (ROW_FRICTION) */
+  int type;
+  int closed;                /* free key limit row (solved in closed form) */
 } row;
-
-/* Row identity: hand limit (dof, side), key limit (key, side), contact edge (capsule, key or
- * base or capsule, capsule-box sub-contact, pyramid edge). */
-static uint32_t row_id_limit(int dof, int side) { return (0u << 30) | ((uint32_t)dof << 1) | (uint32_t)side; }
-static uint32_t row_id_key(int key, int side) { return (1u << 30) | ((uint32_t)key << 1) | (uint32_t)side; }
-static uint32_t row_id_contact(const contact* c, int edge) {
-  uint32_t cid = c->kind == 2 ? (uint32_t)(NH * NG * (NK + 1) * 3 + c->g1 * NH * NG + c->g2)
-                              : (uint32_t)((c->g2 * (NK + 1) + (c->key < 0 ? NK : c->key)) * 4 + c->sub);
-  return (2u << 30) | (cid << 2) | (uint32_t)edge;
-}
 
 static double impedance(const double* si, double pos) {
   double d0 = clampd(si[0], MINIMP, MAXIMP), dw = clampd(si[1], MINIMP, MAXIMP);
@@ -1153,25 +1145,18 @@ static double dotv(const double* a, const double* b) {
   return s;
 }
 
-/* diagApprox: MuJoCo's constant regulariser scale from invweight0 (mj_diagApprox) */
+/* aref and R of a row (mj_makeImpedance / mj_makeKBIP): pos = the row's violation (0 for
+ * friction loss), diag_approx = MuJoCo's constant regulariser scale from invweight0 */
 static void row_finish(const model* m, envdata* E, row* r, double pos, const double* solref, const double* solimp,
-                       double diag_approx, const double* qacc_smooth) {
+                       double diag_approx) {
   const ps_model_desc* d = &m->d;
-  memcpy(r->y, r->J, sizeof(r->y));
-  for (int h = 0; h < NH; h++) solve_LT(m, h, E->M[h], r->y + NK + h * ND);
-  double A = 0;
-  for (int k = 0; k < NK; k++) A += r->y[k] * r->y[k] / E->Mk[k];
-  for (int h = 0; h < NH; h++)
-    for (int j = 0; j < ND; j++) A += r->y[NK + h * ND + j] * r->y[NK + h * ND + j] / E->D[h][j];
-  r->Aii = A;
   double imp = impedance(solimp, pos);
   double dmax = clampd(solimp[1], MINIMP, MAXIMP);
   double tc = fmax(solref[0], 2.0 * d->timestep), dr = solref[1];
   double K = 1.0 / (dmax * dmax * tc * tc * dr * dr), B = 2.0 / (dmax * tc);
   r->aref = -B * dotv(r->J, E->v) - K * imp * pos;
   r->R = fmax(MINVAL, (1.0 - imp) / imp * diag_approx);
-  r->b = dotv(r->J, qacc_smooth) - r->aref;
-  r->f = 0;
+  r->D = 1.0 / r->R;
 }
 
 static void mix_param(const ps_contact_param* a, const ps_contact_param* b, double* solref, double* solimp, double* mu) {
@@ -1180,319 +1165,434 @@ static void mix_param(const ps_contact_param* a, const ps_contact_param* b, doub
   *mu = fmax(a->friction, b->friction);
 }
 
+#define MAXROW (NH * ND + NH * ND + 2 * NK + 4 * MAXCON)  /* friction loss, limits, contacts: no cap */
 static _Thread_local row g_rows[MAXROW];
 int ref_debug_level = 0;
-long ref_rows_hist[PS_MAX_ROWS + 2];
-long ref_con_hist[PS_MAX_CONTACTS_LIMIT + 2];
-/* Cap study (per substep): contacts the narrow phase found (kept or not) and coupled rows
- * requested (before the PS_MAX_ROWS cap), each clamped into the last bin; substeps where a
- * cap dropped something; sweeps the PGS ran. */
+/* Per-substep study histograms: contacts the narrow phase found (kept or not), constraint
+ * rows, contacts kept; substeps where the contact cap dropped a contact. */
 #define REF_HIST 256
+long ref_rows_hist[REF_HIST];
+long ref_con_hist[PS_MAX_CONTACTS_LIMIT + 2];
 long ref_found_hist[REF_HIST];
-long ref_rowreq_hist[REF_HIST];
-long ref_cap_events[2];  /* [0] substeps with contacts dropped, [1] with rows dropped */
-long ref_sweeps_total, ref_substeps_total;
-/* Study override of the constraint solve (the specification is cfg->solver, see
- * dual_solve below):
- *   0: none (the specification);
- *   1: PGS run to convergence from a cold start - at least cfg->pgs_iterations sweeps, then
- *      until a sweep changes no force by more than ref_pgs_tol * (1 + max|f|), at most
- *      ref_pgs_maxit sweeps. An independent check of the exact solve: the dual is strictly
- *      convex (R > 0), so both reach the same unique solution. */
+long ref_cap_events[1];
+long ref_iter_total, ref_substeps_total;
+long ref_newton_hist[64];     /* Newton iterations per substep ([63]: iteration cap) */
+long ref_warnings_total[PS_NWARN];
+/* Study override of the constraint solve:
+ *   0: the specification (primal Newton, below);
+ *   1: projected Gauss-Seidel on the dual, from a cold start until a sweep changes no force by
+ *      more than ref_pgs_tol * (1 + max|f|) (at most ref_pgs_maxit sweeps): an independent
+ *      method for the same unique solution (the dual of a strictly convex problem). */
 int ref_pgs_mode = 0;
+int ref_warmstart = 0;
+int ref_fullstep = 0;   /* study: full Newton steps when they descend */  /* study: Newton from qacc_warmstart (MuJoCo's rule) instead of qacc_smooth */
 double ref_pgs_tol = 1e-12;
 int ref_pgs_maxit = 200000;
-long ref_pdas_hist[64];
-FILE* ref_qp_dump;  /* study: append every coupled-row QP here (NULL: off) */  /* linear solves per substep of the exact solve ([63]: iteration cap) */
-#include <stdio.h>
 
-/* Delassus entry of coupled rows i, j: y_i D^-1 y_j (keys: 1 / (I + armature)). */
-static double delassus(const envdata* E, const row* a, const row* b) {
-  double s = 0;
-  for (int k = 0; k < NK; k++) s += a->y[k] * b->y[k] / E->Mk[k];
-  for (int h = 0; h < NH; h++)
-    for (int j = 0; j < ND; j++) s += a->y[NK + h * ND + j] * b->y[NK + h * ND + j] / E->D[h][j];
-  return s;
+/* s'(jar) of a row: the negative of its constraint force. Unilateral rows (limits, pyramid
+ * edges): D jar while jar < 0, else 0. Friction loss: D jar clamped to [-floss, floss] (the
+ * quadratic zone |jar| < R floss, the two linear zones outside) - MuJoCo's
+ * mj_constraintUpdate states QUADRATIC / SATISFIED / LINEARNEG / LINEARPOS. */
+static double row_dcost(const row* r, double jar) {
+  double t = r->D * jar;
+  if (r->type == ROW_FRICTION) return clampd(t, -r->floss, r->floss);
+  return t < 0.0 ? t : 0.0;
+}
+static double row_cost(const row* r, double jar) {
+  if (r->type == ROW_FRICTION) {
+    double z = r->R * r->floss;
+    if (jar <= -z) return -r->floss * (jar + 0.5 * z);
+    if (jar >= z) return r->floss * (jar - 0.5 * z);
+    return 0.5 * r->D * jar * jar;
+  }
+  return jar < 0.0 ? 0.5 * r->D * jar * jar : 0.0;
+}
+/* 1: the row is in its quadratic zone (contributes D J'J to the Hessian) */
+static int row_quad(const row* r, double jar) {
+  if (r->type == ROW_FRICTION) return fabs(jar) < r->R * r->floss;
+  return jar < 0.0;
 }
 
-#define REF_BIG_SWEEPS 2  /* kernel_v2.inc PS_BIG_SWEEPS */
-#define BPP_MAXIT 32
-#define BPP_TOL 1e-10  /* infeasibility below this fraction of max|f| (f) or max|b| (w) is rounding */
-/* Exact solve of the coupled rows' dual problem
- *     min_f 1/2 f'Hf + b'f   s.t. f >= 0,   H = A + diag(R),  A = J M^-1 J' (Delassus),
- * the linear complementarity problem w = Hf + b, f >= 0, w >= 0, f'w = 0. Its solution is
- * unique (H positive definite) and is the constraint force MuJoCo's solvers converge to on
- * these rows (the default Newton solver minimises the equivalent primal in qacc; pyramidal
- * cones make every row unilateral).
- * Method: block principal pivoting (Judice & Pires 1994; Kim & Park's NNLS form): a free set
- * F gives f_F = -H_FF^-1 b_F (LDL' factorization of H_FF), f = 0 and w = Hf + b elsewhere;
- * the infeasible rows V = {i in F: f_i < 0} u {i not in F: w_i < 0} are exchanged all at
- * once while |V| keeps decreasing (3 backup exchanges allowed), otherwise only the largest
- * index of V (Murty's rule), which terminates for any positive definite H. V empty = the
- * solution. The start F = {f_i - w_i/H_ii > 0} is the free set of the forces on entry (the
- * cfg->pgs_iterations warm-up sweeps; with none, {b_i < 0}). Returns the number of solves,
- * or -1 when BPP_MAXIT solves did not finish (forces = max(0, last iterate)). */
-/* LDL' solve of H_FF x_F = -b_F for the rows fi[0..m) (x = 0 elsewhere) */
-static void solve_free(int n, int m, const int* fi, double H[][MAXROW], const double* bb, double* x) {
-  static _Thread_local double L[MAXROW][MAXROW];
-  double dg[MAXROW], z[MAXROW];
-  for (int a = 0; a < m; a++)
-    for (int c = 0; c <= a; c++) L[a][c] = H[fi[a]][fi[c]];
-  for (int k = 0; k < m; k++) {  /* right-looking LDL' (L unit lower) */
-    dg[k] = L[k][k];
-    for (int a = k + 1; a < m; a++) {
-      double l = L[a][k] / dg[k];
-      for (int c = k + 1; c <= a; c++) L[a][c] -= l * L[c][k];
+/* Primal Newton solve of the constraint forces (MuJoCo's default solver, mj_solNewton):
+ *     min_x  1/2 (x - x_s)' M (x - x_s) + sum_r s_r(J_r x - aref_r)
+ * over the accelerations x of the coupled dofs (both hands and the keys touched by a
+ * contact), x_s = qacc_smooth. The cost is strictly convex and piecewise quadratic, so its
+ * minimiser is unique - the one every MuJoCo solver converges to. Iteration: Newton direction
+ * from the Hessian M + sum_{quadratic rows} D_r J_r' J_r (dense Cholesky over the coupled
+ * dofs), then the EXACT line search along it (the derivative of the piecewise-quadratic cost
+ * along the direction is piecewise linear and non-decreasing: its root is found by walking the
+ * sorted breakpoints), until the gradient vanishes to 1e-13 relative. Returns the iterations,
+ * -1 at the cap. x enters as x_s and leaves as qacc. */
+#define NEWTON_MAXIT 100
+#define NEWTON_TOL 1e-13
+static int newton_solve(const model* m, envdata* E, int nr, const int* dofs, int nd, const double* xs, double* x) {
+  static _Thread_local double H[NV][NV], jar[MAXROW], jdir[MAXROW];
+  double g[NV], dx[NV], y[NV];
+  int ret = -1;
+  for (int iter = 1; iter <= NEWTON_MAXIT; iter++) {
+    /* residuals, gradient M (x - x_s) + J' s'(jar) */
+    for (int i = 0; i < NV; i++) y[i] = x[i] - xs[i];
+    double gscale = 0.0;
+    for (int a = 0; a < nd; a++) {
+      int i = dofs[a];
+      double s = 0.0, sa = 0.0;  /* sa: the rounding scale of s, sum |M_ij| (|x_j| + |x_s,j|) */
+      if (i < NK) { s = E->Mk[i] * y[i]; sa = E->Mk[i] * (fabs(x[i]) + fabs(xs[i])); }
+      else {
+        int h = (i - NK) / ND, ii = (i - NK) % ND;
+        for (int jj = 0; jj < ND; jj++) {
+          s += E->Mfull[h][ii][jj] * y[NK + h * ND + jj];
+          sa += fabs(E->Mfull[h][ii][jj]) * (fabs(x[NK + h * ND + jj]) + fabs(xs[NK + h * ND + jj]));
+        }
+      }
+      g[i] = s;
+      gscale = fmax(gscale, sa);
     }
-    for (int a = k + 1; a < m; a++) L[a][k] /= dg[k];
-  }
-  for (int a = 0; a < m; a++) {
-    double s = -bb[fi[a]];
-    for (int k = 0; k < a; k++) s -= L[a][k] * z[k];
-    z[a] = s;
-  }
-  for (int a = 0; a < m; a++) z[a] /= dg[a];
-  for (int a = m - 1; a >= 0; a--) {
-    double s = z[a];
-    for (int k = a + 1; k < m; k++) s -= L[k][a] * z[k];
-    z[a] = s;
-  }
-  for (int i = 0; i < n; i++) x[i] = 0.0;
-  for (int a = 0; a < m; a++) x[fi[a]] = z[a];
-}
-
-static int dual_solve(envdata* E, int nr) {
-  int idx[MAXROW], n = 0;
-  for (int i = 0; i < nr; i++)
-    if (!g_rows[i].closed) idx[n++] = i;
-  if (n == 0) { E->prev_n = 0; return 0; }
-  static _Thread_local double H[MAXROW][MAXROW];
-  double bb[MAXROW], f[MAXROW], x[MAXROW], wv[MAXROW];
-  int inF[MAXROW], fi[MAXROW];
-  double bscale = 0.0;
-  for (int i = 0; i < n; i++) {
-    const row* ri = &g_rows[idx[i]];
-    for (int j = 0; j <= i; j++) H[i][j] = H[j][i] = delassus(E, ri, &g_rows[idx[j]]);
-    H[i][i] += ri->R;
-    bb[i] = ri->b;
-    bscale = fmax(bscale, fabs(bb[i]));
-    f[i] = ri->f;  /* after the warm-up sweeps (0 without) */
-  }
-  const double wtol = BPP_TOL * bscale;
-  /* start: the free set of the warm-up forces, F = {f_i - w_i / H_ii > 0} (with no warm-up
-   * sweeps: {b_i < 0}) - the HIP kernel's rule */
-  for (int i = 0; i < n; i++) {
-    double s = bb[i];
-    for (int j = 0; j < n; j++) s += H[i][j] * f[j];
-    inF[i] = f[i] - s / H[i][i] > 0.0;
-  }
-  if (ref_qp_dump) {  /* study: n, H (n x n), b, warm-up f, start set */
-    int32_t nn = n;
-    fwrite(&nn, 4, 1, ref_qp_dump);
-    for (int i = 0; i < n; i++) fwrite(H[i], sizeof(double), n, ref_qp_dump);
-    fwrite(bb, sizeof(double), n, ref_qp_dump);
-    fwrite(f, sizeof(double), n, ref_qp_dump);
-    for (int i = 0; i < n; i++) { double v = inF[i]; fwrite(&v, sizeof(double), 1, ref_qp_dump); }
-  }
-  int ninf = n + 1, backup = 3, ret = -1;
-  for (int iter = 1; iter <= BPP_MAXIT; iter++) {
-    int m = 0;
-    for (int i = 0; i < n; i++)
-      if (inF[i]) fi[m++] = i;
-    solve_free(n, m, fi, H, bb, x);
-    double xscale = 0.0;
-    for (int i = 0; i < n; i++) xscale = fmax(xscale, fabs(x[i]));
-    const double ftol = BPP_TOL * xscale;
-    int nv = 0, last = -1;
-    for (int i = 0; i < n; i++) {
-      double s = bb[i];
-      for (int j = 0; j < n; j++) s += H[i][j] * x[j];
-      wv[i] = s;
-      if (inF[i] ? x[i] < -ftol : wv[i] < -wtol) { nv++; last = i; }
+    double fscale = 0.0;
+    for (int r = 0; r < nr; r++) {
+      if (g_rows[r].closed) continue;
+      jar[r] = dotv(g_rows[r].J, x) - g_rows[r].aref;
+      double ds = row_dcost(&g_rows[r], jar[r]);
+      if (ds != 0.0)
+        for (int a = 0; a < nd; a++) g[dofs[a]] += g_rows[r].J[dofs[a]] * ds;
+      for (int a = 0; a < nd; a++) fscale = fmax(fscale, fabs(g_rows[r].J[dofs[a]] * ds));
     }
-    if (nv == 0) { ret = iter; break; }
-    if (nv < ninf) { ninf = nv; backup = 3; }
-    else if (backup > 0) backup--;
-    else { inF[last] = !inF[last]; continue; }
-    for (int i = 0; i < n; i++)
-      if (inF[i] ? x[i] < -ftol : wv[i] < -wtol) inF[i] = !inF[i];
-  }
-  E->prev_n = n;
-  for (int i = 0; i < n; i++) {
-    g_rows[idx[i]].f = ret > 0 ? x[i] : fmax(0.0, x[i]);
-    E->prev_id[i] = g_rows[idx[i]].id;
-    E->prev_free[i] = g_rows[idx[i]].f > 0.0;
+    double gmax = 0.0;
+    for (int a = 0; a < nd; a++) gmax = fmax(gmax, fabs(g[dofs[a]]));
+    if (ref_debug_level == 7 || (ref_debug_level == 8 && iter > 90)) printf("iter %d gmax %.3e scale %.3e %.3e\n", iter, gmax, gscale, fscale);
+    if (gmax <= NEWTON_TOL * fmax(fmax(gscale, fscale), 1e-300)) { ret = iter - 1; break; }
+    /* Hessian over the coupled dofs */
+    for (int a = 0; a < nd; a++)
+      for (int b = 0; b < nd; b++) {
+        int i = dofs[a], j = dofs[b];
+        double v = 0.0;
+        if (i < NK || j < NK) v = i == j ? E->Mk[i] : 0.0;
+        else if ((i - NK) / ND == (j - NK) / ND) v = E->Mfull[(i - NK) / ND][(i - NK) % ND][(j - NK) % ND];
+        H[a][b] = v;
+      }
+    for (int r = 0; r < nr; r++) {
+      if (g_rows[r].closed || !row_quad(&g_rows[r], jar[r])) continue;
+      const double* J = g_rows[r].J;
+      for (int a = 0; a < nd; a++) {
+        double ja = J[dofs[a]];
+        if (ja == 0.0) continue;
+        for (int b = 0; b < nd; b++) H[a][b] += g_rows[r].D * ja * J[dofs[b]];
+      }
+    }
+    /* Cholesky H = L L' in place (lower), then dx = -H^-1 g */
+    for (int k = 0; k < nd; k++) {
+      double s = H[k][k];
+      for (int c = 0; c < k; c++) s -= H[k][c] * H[k][c];
+      H[k][k] = sqrt(fmax(s, MINVAL));
+      for (int a = k + 1; a < nd; a++) {
+        double t = H[a][k];
+        for (int c = 0; c < k; c++) t -= H[a][c] * H[k][c];
+        H[a][k] = t / H[k][k];
+      }
+    }
+    double z[NV];
+    for (int a = 0; a < nd; a++) {
+      double s = -g[dofs[a]];
+      for (int c = 0; c < a; c++) s -= H[a][c] * z[c];
+      z[a] = s / H[a][a];
+    }
+    for (int a = nd - 1; a >= 0; a--) {
+      double s = z[a];
+      for (int c = a + 1; c < nd; c++) s -= H[c][a] * z[c];
+      z[a] = s / H[a][a];
+    }
+    memset(dx, 0, sizeof(dx));
+    for (int a = 0; a < nd; a++) dx[dofs[a]] = z[a];
+    /* exact line search: phi'(t) = t dx'M dx + dx'M y + sum_r jdir_r s_r'(jar_r + t jdir_r) */
+    double q2 = 0.0, q1 = 0.0;
+    for (int a = 0; a < nd; a++) {
+      int i = dofs[a];
+      double s = 0.0;
+      if (i < NK) s = E->Mk[i] * dx[i];
+      else {
+        int h = (i - NK) / ND, ii = (i - NK) % ND;
+        for (int jj = 0; jj < ND; jj++) s += E->Mfull[h][ii][jj] * dx[NK + h * ND + jj];
+      }
+      q2 += dx[i] * s;
+      q1 += y[i] * s;
+    }
+    double bp[2 * MAXROW];
+    int nbp = 0;
+    for (int r = 0; r < nr; r++) {
+      if (g_rows[r].closed) continue;
+      jdir[r] = dotv(g_rows[r].J, dx);
+      if (jdir[r] == 0.0) continue;
+      if (g_rows[r].type == ROW_FRICTION) {
+        double z0 = g_rows[r].R * g_rows[r].floss;
+        double t1 = (-z0 - jar[r]) / jdir[r], t2 = (z0 - jar[r]) / jdir[r];
+        if (t1 > 0.0) bp[nbp++] = t1;
+        if (t2 > 0.0) bp[nbp++] = t2;
+      } else {
+        double t = -jar[r] / jdir[r];
+        if (t > 0.0) bp[nbp++] = t;
+      }
+    }
+    for (int i = 1; i < nbp; i++) {  /* insertion sort (breakpoints are few) */
+      double v = bp[i];
+      int k = i - 1;
+      while (k >= 0 && bp[k] > v) { bp[k + 1] = bp[k]; k--; }
+      bp[k + 1] = v;
+    }
+    /* phi' is linear between breakpoints: evaluate it at the left end of each segment and at
+     * a point inside it; the root is in the first segment whose right end has phi' >= 0 */
+    double t_lo = 0.0, alpha = -1.0;
+    for (int s = 0; s <= nbp && alpha < 0.0; s++) {
+      double t_hi = s < nbp ? bp[s] : (t_lo > 0.0 ? 2.0 * t_lo + 1.0 : 1.0);
+      if (t_hi <= t_lo) continue;
+      double tm = 0.5 * (t_lo + t_hi);
+      /* within (t_lo, t_hi) every row keeps its zone: phi'(t) = c0 + c1 t */
+      double c1 = q2, c0 = q1;
+      for (int r = 0; r < nr; r++) {
+        if (g_rows[r].closed || jdir[r] == 0.0) continue;
+        const row* rr = &g_rows[r];
+        double jm = jar[r] + tm * jdir[r];
+        if (row_quad(rr, jm)) {
+          c1 += rr->D * jdir[r] * jdir[r];
+          c0 += rr->D * jdir[r] * jar[r];
+        } else {
+          c0 += jdir[r] * row_dcost(rr, jm);
+        }
+      }
+      double root = c1 > 0.0 ? -c0 / c1 : (c0 < 0.0 ? 1e300 : t_lo);
+      if (s == nbp) alpha = fmax(root, t_lo);  /* last segment is unbounded */
+      else if (root <= t_hi) alpha = fmax(root, t_lo);
+      t_lo = t_hi;
+    }
+    if (ref_debug_level == 7 || (ref_debug_level == 8 && iter > 90)) printf("   alpha %.6g nbp %d q2 %.3e q1 %.3e\n", alpha, nbp, q2, q1);
+    if (ref_fullstep) {  /* study: the full Newton step whenever it lowers the cost */
+      double c0 = 0.5 * 0.0, c1 = 0.5 * q2 + q1;  /* quadratic part: f(t) - f(0) = t^2/2 q2 + t q1 */
+      for (int r = 0; r < nr; r++) {
+        if (g_rows[r].closed) continue;
+        c0 += row_cost(&g_rows[r], jar[r]);
+        c1 += row_cost(&g_rows[r], jar[r] + jdir[r]);
+      }
+      if (c1 < c0) alpha = 1.0;
+    }
+    double step = 0.0, xmag = 0.0;
+    for (int a = 0; a < nd; a++) {
+      x[dofs[a]] += alpha * dx[dofs[a]];
+      step = fmax(step, fabs(alpha * dx[dofs[a]]));
+      xmag = fmax(xmag, fabs(x[dofs[a]]));
+    }
+    if (step <= 1e-15 * xmag) { ret = iter; break; }  /* at the rounding floor of x */
+    (void)row_cost;
   }
   return ret;
+}
+
+/* Dual projected Gauss-Seidel run to convergence (study mode 1): rows' Delassus entries
+ * J M^-1 J' from the tree factor, boxes [-floss, floss] for friction loss, f >= 0 otherwise. */
+static void dual_pgs(const model* m, envdata* E, int nr, const double* xs, double* f) {
+  static _Thread_local double Y[MAXROW][NV];  /* M^-1 J' */
+  double A[MAXROW], b[MAXROW];
+  for (int r = 0; r < nr; r++) {
+    solve_full(m, E, 0, g_rows[r].J, Y[r]);
+    A[r] = dotv(g_rows[r].J, Y[r]);
+    b[r] = dotv(g_rows[r].J, xs) - g_rows[r].aref;
+    f[r] = 0.0;
+  }
+  double acc[NV];  /* M^-1 J' f */
+  memset(acc, 0, sizeof(acc));
+  for (int it = 0; it < ref_pgs_maxit; it++) {
+    double dfmax = 0.0, fmaxabs = 0.0;
+    for (int r = 0; r < nr; r++) {
+      if (g_rows[r].closed) continue;
+      double res = b[r] + g_rows[r].R * f[r] + dotv(g_rows[r].J, acc);
+      double fn = f[r] - res / (A[r] + g_rows[r].R);
+      fn = g_rows[r].type == ROW_FRICTION ? clampd(fn, -g_rows[r].floss, g_rows[r].floss) : fmax(0.0, fn);
+      double df = fn - f[r];
+      if (df != 0.0)
+        for (int k = 0; k < NV; k++) acc[k] += Y[r][k] * df;
+      f[r] = fn;
+      dfmax = fmax(dfmax, fabs(df));
+      fmaxabs = fmax(fmaxabs, fabs(fn));
+    }
+    __atomic_fetch_add(&ref_iter_total, 1, __ATOMIC_RELAXED);
+    if (dfmax <= ref_pgs_tol * (1.0 + fmaxabs)) break;
+  }
+}
+
+static void reset_physics(envdata* E, int warning) {
+  /* mj_resetData after mj_checkPos / mj_checkVel / mj_checkAcc: qpos = qpos0 (0 here), qvel,
+   * qacc_warmstart, ctrl and qfrc_applied = 0; the warning counts survive (dm_control's
+   * check_invalid_state compares them around the step) */
+  memset(E->q, 0, sizeof(E->q));
+  memset(E->v, 0, sizeof(E->v));
+  memset(E->qacc_ws, 0, sizeof(E->qacc_ws));
+  memset(E->ctrl, 0, sizeof(E->ctrl));
+  memset(E->applied, 0, sizeof(E->applied));
+  E->warnings[warning]++;
+  __atomic_fetch_add(&ref_warnings_total[warning], 1, __ATOMIC_RELAXED);
+}
+/* mju_isBad: NaN or |x| > mjMAXVAL (1e10) */
+static int bad_vec(const double* x, int n) {
+  for (int i = 0; i < n; i++)
+    if (!(fabs(x[i]) <= 1e10)) return 1;
+  return 0;
 }
 
 static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
   const ps_model_desc* d = &m->d;
   const double h_t = d->timestep;
-  kinematics(m, E);
-  dynamics(m, cfg, E);
-  collide(m, cfg, E);
-  for (int h = 0; h < NH; h++) {
-    memcpy(E->Mh[h], E->M[h], sizeof(E->M[h]));
-    for (int j = 0; j < ND; j++) E->Mh[h][j][j] += h_t * d->dof_damping[h][j];
-    factor(m, h, E->M[h], E->D[h]);
-    factor(m, h, E->Mh[h], E->Dh[h]);
-  }
-  double fsmooth[NV], qacc_smooth[NV];
-  for (int i = 0; i < NV; i++) fsmooth[i] = E->passive[i] + E->actfrc[i] + E->applied[i] - E->bias[i];
-  solve_full(m, E, 0, fsmooth, qacc_smooth);
+  /* mj_checkPos, mj_checkVel (mj_step1) */
+  if (bad_vec(E->q, NV)) reset_physics(E, PS_WARN_BADQPOS);
+  if (bad_vec(E->v, NV)) reset_physics(E, PS_WARN_BADQVEL);
+  for (int pass = 0; pass < 2; pass++) {  /* pass 1: after mj_checkAcc reset the state */
+    kinematics(m, E);
+    dynamics(m, cfg, E);
+    collide(m, cfg, E);
+    for (int h = 0; h < NH; h++) {
+      memcpy(E->Mfull[h], E->M[h], sizeof(E->M[h]));
+      memcpy(E->Mh[h], E->M[h], sizeof(E->M[h]));
+      for (int j = 0; j < ND; j++) E->Mh[h][j][j] += h_t * d->dof_damping[h][j];
+      factor(m, h, E->M[h], E->D[h]);
+      factor(m, h, E->Mh[h], E->Dh[h]);
+    }
+    double fsmooth[NV], qacc_smooth[NV];
+    for (int i = 0; i < NV; i++) fsmooth[i] = E->passive[i] + E->actfrc[i] + E->applied[i] - E->bias[i];
+    solve_full(m, E, 0, fsmooth, qacc_smooth);
 
-  /* constraint rows: hand limits, key limits (coupled first, free ones closed-form), contacts */
-  int keyhit[NK];
-  memset(keyhit, 0, sizeof(keyhit));
-  for (int c = 0; c < E->ncon; c++)
-    if (E->con[c].kind == 0) keyhit[E->con[c].key] = 1;
-  int nr = 0, ncoup = 0;  /* coupled rows are capped at PS_MAX_ROWS, later ones dropped */
-  int nreq = 4 * E->ncon;  /* coupled rows requested before the cap */
-  for (int h = 0; h < NH; h++)
-    for (int j = 0; j < ND; j++) {
-      if (!d->dof_limited[h][j]) continue;
-      double q = E->q[NK + h * ND + j];
-      for (int side = 0; side < 2; side++) {
-        double dist = side == 0 ? q - d->dof_range[h][j][0] : d->dof_range[h][j][1] - q;
-        if (dist < 0.0) nreq++;
-        if (dist >= 0.0 || ncoup >= PS_MAX_ROWS) continue;
-        ncoup++;
+    /* rows: friction loss (hand dofs), hand limits, key limits (keys touched by a contact are
+     * coupled; the others are 1-dof problems solved in closed form), contacts (4 pyramid
+     * edges each). No row cap. */
+    int keyhit[NK];
+    memset(keyhit, 0, sizeof(keyhit));
+    for (int c = 0; c < E->ncon; c++)
+      if (E->con[c].kind == 0) keyhit[E->con[c].key] = 1;
+    int nr = 0;
+    for (int h = 0; h < NH; h++)
+      for (int j = 0; j < ND; j++) {
+        if (!(d->dof_frictionloss[h][j] > 0.0)) continue;
         row* r = &g_rows[nr++];
         memset(r->J, 0, sizeof(r->J));
-        r->J[NK + h * ND + j] = side == 0 ? 1.0 : -1.0;
+        r->J[NK + h * ND + j] = 1.0;
+        r->type = ROW_FRICTION;
         r->closed = 0;
-        r->id = row_id_limit(h * ND + j, side);
-        row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->dof_invweight[h][j], qacc_smooth);
+        r->floss = d->dof_frictionloss[h][j];
+        row_finish(m, E, r, 0.0, d->friction_solref, d->friction_solimp, d->dof_invweight[h][j]);
       }
-    }
-  for (int pass = 0; pass < 2; pass++)
-    for (int k = 0; k < NK; k++) {
-      if ((pass == 0) != (keyhit[k] != 0)) continue;
+    for (int h = 0; h < NH; h++)
+      for (int j = 0; j < ND; j++) {
+        if (!d->dof_limited[h][j]) continue;
+        double q = E->q[NK + h * ND + j];
+        for (int side = 0; side < 2; side++) {
+          double dist = side == 0 ? q - d->dof_range[h][j][0] : d->dof_range[h][j][1] - q;
+          if (dist >= 0.0) continue;
+          row* r = &g_rows[nr++];
+          memset(r->J, 0, sizeof(r->J));
+          r->J[NK + h * ND + j] = side == 0 ? 1.0 : -1.0;
+          r->type = ROW_LIMIT;
+          r->closed = 0;
+          row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->dof_invweight[h][j]);
+        }
+      }
+    for (int k = 0; k < NK; k++)
       for (int side = 0; side < 2; side++) {
         double dist = side == 0 ? E->q[k] - d->key_range[k][0] : d->key_range[k][1] - E->q[k];
         if (dist >= 0.0) continue;
-        if (pass == 0) {
-          nreq++;
-          if (ncoup >= PS_MAX_ROWS) continue;
-          ncoup++;
-        }
         row* r = &g_rows[nr++];
         memset(r->J, 0, sizeof(r->J));
         r->J[k] = side == 0 ? 1.0 : -1.0;
-        r->closed = pass;
-        r->id = row_id_key(k, side);
-        row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->key_dof_invweight[k], qacc_smooth);
+        r->type = ROW_LIMIT;
+        r->closed = !keyhit[k];
+        row_finish(m, E, r, dist, d->limit_solref, d->limit_solimp, d->key_dof_invweight[k]);
+      }
+    for (int c = 0; c < E->ncon; c++) {
+      contact* cc = &E->con[c];
+      double solref[2], solimp[5], mu;
+      mix_param(cc->kind == 2 ? &d->hand_contact : &d->piano_contact, &d->hand_contact, solref, solimp, &mu);
+      double Jn[NV], Jt1[NV], Jt2[NV];
+      contact_jac(m, E, cc, cc->n, Jn);
+      contact_jac(m, E, cc, cc->t1, Jt1);
+      contact_jac(m, E, cc, cc->t2, Jt2);
+      double tran = d->body_invweight[cc->h2][cc->b2];
+      if (cc->kind == 0) tran += d->key_body_invweight[cc->key];
+      else if (cc->kind == 2) tran += d->body_invweight[cc->h1][cc->b1];
+      double diag = (1.0 + mu * mu) * tran;
+      for (int e = 0; e < 4; e++) {
+        row* r = &g_rows[nr++];
+        const double* Jt = e < 2 ? Jt1 : Jt2;
+        double s = (e & 1) ? -mu : mu;
+        for (int i = 0; i < NV; i++) r->J[i] = Jn[i] + s * Jt[i];
+        r->type = ROW_CONTACT;
+        r->closed = 0;
+        row_finish(m, E, r, cc->dist, solref, solimp, diag);
       }
     }
-  for (int c = 0; c < E->ncon; c++) {
-    if (ncoup + 4 > PS_MAX_ROWS) break;  /* whole contacts only */
-    contact* cc = &E->con[c];
-    double solref[2], solimp[5], mu;
-    mix_param(cc->kind == 2 ? &d->hand_contact : &d->piano_contact, &d->hand_contact, solref, solimp, &mu);
-    double Jn[NV], Jt1[NV], Jt2[NV];
-    contact_jac(m, E, cc, cc->n, Jn);
-    contact_jac(m, E, cc, cc->t1, Jt1);
-    contact_jac(m, E, cc, cc->t2, Jt2);
-    double tran = d->body_invweight[cc->h2][cc->b2];
-    if (cc->kind == 0) tran += d->key_body_invweight[cc->key];
-    else if (cc->kind == 2) tran += d->body_invweight[cc->h1][cc->b1];
-    double diag = (1.0 + mu * mu) * tran;
-    for (int e = 0; e < 4; e++) {
-      ncoup++;
-      row* r = &g_rows[nr++];
-      const double* Jt = e < 2 ? Jt1 : Jt2;
-      double s = (e & 1) ? -mu : mu;
-      for (int i = 0; i < NV; i++) r->J[i] = Jn[i] + s * Jt[i];
-      r->closed = 0;
-      r->id = row_id_contact(cc, e);
-      row_finish(m, E, r, cc->dist, solref, solimp, diag, qacc_smooth);
-    }
-  }
+    __atomic_fetch_add(&ref_rows_hist[nr < REF_HIST ? nr : REF_HIST - 1], 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&ref_con_hist[E->ncon], 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&ref_found_hist[E->nfound < REF_HIST ? E->nfound : REF_HIST - 1], 1, __ATOMIC_RELAXED);
+    if (E->nfound > E->ncon) __atomic_fetch_add(&ref_cap_events[0], 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&ref_substeps_total, 1, __ATOMIC_RELAXED);
 
-  __atomic_fetch_add(&ref_rows_hist[ncoup], 1, __ATOMIC_RELAXED); /* ref_step_threads runs envs in parallel */
-  __atomic_fetch_add(&ref_con_hist[E->ncon], 1, __ATOMIC_RELAXED);
-  __atomic_fetch_add(&ref_found_hist[E->nfound < REF_HIST ? E->nfound : REF_HIST - 1], 1, __ATOMIC_RELAXED);
-  __atomic_fetch_add(&ref_rowreq_hist[nreq < REF_HIST ? nreq : REF_HIST - 1], 1, __ATOMIC_RELAXED);
-  if (E->nfound > E->ncon) __atomic_fetch_add(&ref_cap_events[0], 1, __ATOMIC_RELAXED);
-  if (nreq > ncoup) __atomic_fetch_add(&ref_cap_events[1], 1, __ATOMIC_RELAXED);
-  /* PGS on the coupled rows; closed-form free key rows */
-  double w[NV];
-  memset(w, 0, sizeof(w));
-  for (int i = 0; i < nr; i++) {
-    row* r = &g_rows[i];
-    if (r->closed) { r->f = fmax(0.0, -r->b / (r->Aii + r->R)); continue; }
-    /* cold start: a qacc_warmstart-derived start (f = -D(J qacc_ws - aref)) is unsafe for
-     * contacts that appeared this substep (huge forces where R is small); MuJoCo guards it
-     * with a cost comparison, here the dual starts at 0 (always stable). */
-    r->f = 0.0;
-    for (int k = 0; k < NV; k++) w[k] += r->y[k] * r->f;
-  }
-  /* the exact solve's warm-up: cfg->pgs_iterations sweeps, at most REF_BIG_SWEEPS above 32
-   * coupled rows (the kernel factors those free sets on the matrix cores, where a solve costs
-   * about five sweeps) */
-  int maxit = ref_pgs_mode == 1 ? ref_pgs_maxit : cfg->pgs_iterations, it;
-  if (ref_pgs_mode == 0 && cfg->solver == PS_SOLVER_EXACT && ncoup > 32 && maxit > REF_BIG_SWEEPS) maxit = REF_BIG_SWEEPS;
-  for (it = 0; it < maxit; it++) {
-    double dfmax = 0.0, fmaxabs = 0.0;
-    for (int i = 0; i < nr; i++) {
-      row* r = &g_rows[i];
-      if (r->closed) continue;
-      double res = r->b + r->R * r->f;
-      for (int k = 0; k < NK; k++) res += r->y[k] * w[k] / E->Mk[k];
-      for (int h = 0; h < NH; h++)
-        for (int j = 0; j < ND; j++) res += r->y[NK + h * ND + j] * w[NK + h * ND + j] / E->D[h][j];
-      double fn = fmax(0.0, r->f - res / (r->Aii + r->R));
-      if (ref_debug_level > 1 && i < 4) printf("it %d row %d f %.5g res %.5g fn %.5g\n", it, i, r->f, res, fn);
-      double df = fn - r->f;
-      if (df != 0.0)
-        for (int k = 0; k < NV; k++) w[k] += r->y[k] * df;
-      r->f = fn;
-      if (ref_pgs_mode == 1) {  /* (not in the specification's FLOP count) */
-        if (fabs(df) > dfmax) dfmax = fabs(df);
-        if (fabs(fn) > fmaxabs) fmaxabs = fabs(fn);
+    /* coupled dofs: both hands, then the keys touched by a contact */
+    int dofs[NV], nd = 0;
+    for (int i = NK; i < NV; i++) dofs[nd++] = i;
+    for (int k = 0; k < NK; k++)
+      if (keyhit[k]) dofs[nd++] = k;
+    double x[NV], f[MAXROW];
+    memcpy(x, qacc_smooth, sizeof(x));
+    if (ref_warmstart) {  /* study: MuJoCo's warm start - qacc_warmstart when its cost is lower */
+      double cs = 0.0, cw = 0.0, y[NV];
+      for (int i = 0; i < NV; i++) y[i] = E->qacc_ws[i] - qacc_smooth[i];
+      for (int a = 0; a < nd; a++) {
+        int i = dofs[a];
+        double s = 0.0;
+        if (i < NK) s = E->Mk[i] * y[i];
+        else for (int jj = 0; jj < ND; jj++) s += E->Mfull[(i - NK) / ND][(i - NK) % ND][jj] * y[NK + (i - NK) / ND * ND + jj];
+        cw += 0.5 * y[i] * s;
       }
+      for (int r = 0; r < nr; r++) {
+        if (g_rows[r].closed) continue;
+        cs += row_cost(&g_rows[r], dotv(g_rows[r].J, qacc_smooth) - g_rows[r].aref);
+        cw += row_cost(&g_rows[r], dotv(g_rows[r].J, E->qacc_ws) - g_rows[r].aref);
+      }
+      if (cw < cs)
+        for (int a = 0; a < nd; a++) x[dofs[a]] = E->qacc_ws[dofs[a]];
     }
-    if (ref_pgs_mode == 1 && it + 1 >= cfg->pgs_iterations && dfmax <= ref_pgs_tol * (1.0 + fmaxabs)) {
-      it++;
-      break;
+    if (ref_pgs_mode == 1) {
+      dual_pgs(m, E, nr, qacc_smooth, f);
+    } else {
+      int it = newton_solve(m, E, nr, dofs, nd, qacc_smooth, x);
+      __atomic_fetch_add(&ref_newton_hist[it >= 0 && it < 63 ? it : 63], 1, __ATOMIC_RELAXED);
+      if (it > 0) __atomic_fetch_add(&ref_iter_total, it, __ATOMIC_RELAXED);
+      for (int r = 0; r < nr; r++)
+        if (!g_rows[r].closed) f[r] = -row_dcost(&g_rows[r], dotv(g_rows[r].J, x) - g_rows[r].aref);
     }
-  }
-  __atomic_fetch_add(&ref_sweeps_total, it, __ATOMIC_RELAXED);
-  __atomic_fetch_add(&ref_substeps_total, 1, __ATOMIC_RELAXED);
-  if (ref_pgs_mode == 0 && cfg->solver == PS_SOLVER_EXACT) {
-    int pit = dual_solve(E, nr);
-    __atomic_fetch_add(&ref_pdas_hist[pit >= 0 && pit < 63 ? pit : 63], 1, __ATOMIC_RELAXED);
-    memset(w, 0, sizeof(w));
-    for (int i = 0; i < nr; i++)
-      if (!g_rows[i].closed && g_rows[i].f != 0.0)
-        for (int k = 0; k < NV; k++) w[k] += g_rows[i].y[k] * g_rows[i].f;
-  }
-  for (int i = 0; i < nr; i++)
-    if (g_rows[i].closed)
-      for (int k = 0; k < NK; k++) w[k] += g_rows[i].y[k] * g_rows[i].f;
-  /* qfrc_constraint = J^T f = L^T w */
-  double F[NV];
-  for (int k = 0; k < NK; k++) F[k] = fsmooth[k] + w[k];
-  for (int h = 0; h < NH; h++) {
-    double* wh = w + NK + h * ND;
-    double out[ND];
-    for (int j = 0; j < ND; j++) out[j] = wh[j];
-    for (int k = 0; k < ND; k++)
-      for (int i = m->dof_parent[h][k]; i >= 0; i = m->dof_parent[h][i]) out[i] += E->M[h][k][i] * wh[k];
-    for (int j = 0; j < ND; j++) F[NK + h * ND + j] = fsmooth[NK + h * ND + j] + out[j];
-  }
-  double qacc[NV], qacc_e[NV];
-  solve_full(m, E, 0, F, qacc);
-  if (ref_debug_level) {
-    for (int i = 0; i < nr; i++) if (!g_rows[i].closed)
-      printf("row %d Aii %.4g R %.4g aref %.4g b %.4g f %.4g\n", i, g_rows[i].Aii, g_rows[i].R, g_rows[i].aref, g_rows[i].b, g_rows[i].f);
-  }
-  solve_full(m, E, 1, F, qacc_e);
-  memcpy(E->qacc_ws, qacc, sizeof(qacc));
-  for (int i = 0; i < NV; i++) {
-    E->v[i] += h_t * qacc_e[i];
-    E->q[i] += h_t * E->v[i];
+    /* free key limits: 1-dof problems, f = max(0, -b / (1/Mk + R)) */
+    for (int r = 0; r < nr; r++)
+      if (g_rows[r].closed) {
+        int k = 0;
+        while (g_rows[r].J[k] == 0.0) k++;
+        double b = g_rows[r].J[k] * qacc_smooth[k] - g_rows[r].aref;
+        f[r] = fmax(0.0, -b / (1.0 / E->Mk[k] + g_rows[r].R));
+      }
+    if (ref_debug_level)
+      for (int r = 0; r < nr; r++) printf("row %d type %d R %.4g aref %.4g f %.6g\n", r, g_rows[r].type, g_rows[r].R, g_rows[r].aref, f[r]);
+    /* qfrc_constraint = J' f; qacc = M^-1 (qfrc_smooth + qfrc_constraint) */
+    double F[NV];
+    memcpy(F, fsmooth, sizeof(F));
+    for (int r = 0; r < nr; r++)
+      if (f[r] != 0.0)
+        for (int i = 0; i < NV; i++) F[i] += g_rows[r].J[i] * f[r];
+    double qacc[NV], qacc_e[NV];
+    solve_full(m, E, 0, F, qacc);
+    /* mj_checkAcc: reset and recompute the forward dynamics at the reset state */
+    if (pass == 0 && bad_vec(qacc, NV)) {
+      reset_physics(E, PS_WARN_BADQACC);
+      continue;
+    }
+    solve_full(m, E, 1, F, qacc_e);
+    memcpy(E->qacc_ws, qacc, sizeof(qacc));
+    for (int i = 0; i < NV; i++) {
+      E->v[i] += h_t * qacc_e[i];
+      E->q[i] += h_t * E->v[i];
+    }
+    break;
   }
 }
 
@@ -1581,7 +1681,9 @@ static void key_state(const model* m, envdata* E) {
 }
 
 static void reset_env(ref_env* R, envdata* E, float* obs) {
-  E->hand_dy = R->cfg.randomize_hand_positions ? (double)ref_hand_offset_draw(R->seed, (int)(E - R->e), E->episode) : 0.0;
+  E->hand_dy = R->cfg.randomize_hand_positions
+                    ? (double)ref_hand_offset_draw(R->seed, (int)((uint32_t)R->env_offset + (uint32_t)(E - R->e)), E->episode)
+                    : 0.0;
   E->episode++;
   memset(E->q, 0, sizeof(E->q));
   memset(E->v, 0, sizeof(E->v));
@@ -1627,7 +1729,6 @@ static void control_step(ref_env* R, envdata* E, const float* a, float* obs, flo
   }
   for (int i = 0; i < PS_NU; i++) E->ctrl[i] = a[i];
   E->sustain = a[PS_NU];
-  E->prev_n = 0;  /* the exact solve's warm start lives within one control step (the GPU's LDS) */
   for (int s = 0; s < d->n_substeps; s++) step_physics(m, &R->cfg, E);
   kinematics(m, E);   /* mj_step1 at the final state (legacy_step) */
   collide(m, &R->cfg, E);
@@ -1864,10 +1965,8 @@ void ref_contact_count(const ref_env* R, int32_t* ncon) {
 }
 
 void ref_set_seed(ref_env* R, uint64_t seed) { R->seed = seed; }
-void ref_qp_dump_open(const char* path) {
-  if (ref_qp_dump) fclose(ref_qp_dump);
-  ref_qp_dump = path ? fopen(path, "wb") : NULL;
-}
+/* global id of env 0 (ps_set_env_offset): draws keyed by global env id */
+void ref_set_env_offset(ref_env* R, int64_t off) { R->env_offset = off; }
 void ref_get_hand_offset(const ref_env* R, double* dy, int32_t* episode) {
   for (int i = 0; i < R->n; i++) {
     if (dy) dy[i] = R->e[i].hand_dy;
@@ -1894,23 +1993,27 @@ void ref_stats_reset(void) {
   memset(ref_rows_hist, 0, sizeof(ref_rows_hist));
   memset(ref_con_hist, 0, sizeof(ref_con_hist));
   memset(ref_found_hist, 0, sizeof(ref_found_hist));
-  memset(ref_rowreq_hist, 0, sizeof(ref_rowreq_hist));
   memset(ref_cap_events, 0, sizeof(ref_cap_events));
-  ref_sweeps_total = ref_substeps_total = 0;
-  memset(ref_pdas_hist, 0, sizeof(ref_pdas_hist));
+  memset(ref_newton_hist, 0, sizeof(ref_newton_hist));
+  memset(ref_warnings_total, 0, sizeof(ref_warnings_total));
+  ref_iter_total = ref_substeps_total = 0;
 }
-void ref_pdas_hist_get(long* out) { memcpy(out, ref_pdas_hist, sizeof(ref_pdas_hist)); }
-/* found/rowreq [REF_HIST], kept rows [PS_MAX_ROWS + 2], kept contacts [MAXCON + 2],
- * misc = {substeps with contacts dropped, with rows dropped, sweeps, substeps} */
-void ref_stats_get(long* found, long* rowreq, long* rows, long* cons, long* misc) {
+void ref_newton_hist_get(long* out) { memcpy(out, ref_newton_hist, sizeof(ref_newton_hist)); }
+/* found [REF_HIST], constraint rows [REF_HIST], kept contacts [MAXCON + 2], misc = {substeps
+ * with contacts dropped, solver iterations (Newton) or sweeps (study PGS), substeps, warnings} */
+void ref_stats_get(long* found, long* rows, long* cons, long* misc) {
   memcpy(found, ref_found_hist, sizeof(ref_found_hist));
-  memcpy(rowreq, ref_rowreq_hist, sizeof(ref_rowreq_hist));
   memcpy(rows, ref_rows_hist, sizeof(ref_rows_hist));
   memcpy(cons, ref_con_hist, sizeof(ref_con_hist));
   misc[0] = ref_cap_events[0];
-  misc[1] = ref_cap_events[1];
-  misc[2] = ref_sweeps_total;
-  misc[3] = ref_substeps_total;
+  misc[1] = ref_iter_total;
+  misc[2] = ref_substeps_total;
+  misc[3] = ref_warnings_total[0] + ref_warnings_total[1] + ref_warnings_total[2];
+}
+/* mj_checkPos / Vel / Acc resets of each env since create, [n][PS_NWARN] (ps_warnings) */
+void ref_warnings(const ref_env* R, int32_t* out) {
+  for (int i = 0; i < R->n; i++)
+    for (int w = 0; w < PS_NWARN; w++) out[i * PS_NWARN + w] = R->e[i].warnings[w];
 }
 
 /* Single-substep hook for teacher-forced physics parity (no task layer). */

@@ -54,6 +54,7 @@ def _bind(L):
     L.ref_assignment_tol.argtypes = [C.c_int, C.c_int, _f64p]
     L.ref_set_solver.argtypes = [C.c_int, C.c_double, C.c_int]
     L.ref_set_seed.argtypes = [C.c_void_p, C.c_uint64]
+    L.ref_set_env_offset.argtypes = [C.c_void_p, C.c_int64]
     L.ref_debug_contacts.restype = C.c_int
     L.ref_debug_contacts.argtypes = [C.c_void_p, C.c_int, _i32p, _f64p]
     L.ref_get_hand_offset.argtypes = [C.c_void_p, _f64p, _i32p]
@@ -62,8 +63,9 @@ def _bind(L):
     L.ref_hand_offset_draw.argtypes = [C.c_uint64, C.c_int, C.c_int]
     L.ref_narrow.argtypes = [_f64p, C.c_void_p, C.c_int, _f64p, C.c_void_p, C.c_int, _f64p]
     _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
-    L.ref_stats_get.argtypes = [_i64p] * 5
-    L.ref_pdas_hist_get.argtypes = [_i64p]
+    L.ref_stats_get.argtypes = [_i64p] * 4
+    L.ref_newton_hist_get.argtypes = [_i64p]
+    L.ref_warnings.argtypes = [C.c_void_p, _i32p]
     return L
 
 
@@ -71,8 +73,9 @@ STAT_HIST = 256
 
 
 def set_solver(mode: int = 0, tol: float = 1e-12, maxit: int = 200000, counting: bool = False):
-    """Study override: 0 = the specification (cfg.solver); 1 = PGS run to convergence from a
-    cold start (an independent check of the exact solve; pianosim_ref.c ref_pgs_mode)."""
+    """Study override: 0 = the specification (primal Newton); 1 = dual projected Gauss-Seidel run
+    to convergence from a cold start (an independent method for the same unique solution;
+    pianosim_ref.c ref_pgs_mode)."""
     (flops_lib() if counting else lib()).ref_set_solver(mode, tol, maxit)
 
 
@@ -82,18 +85,18 @@ def stats_reset():
 
 def stats():
     """Per-substep histograms since stats_reset(): contacts found (before the contact cap),
-    coupled rows requested (before PS_MAX_ROWS), rows kept, contacts kept; and the substeps
-    where a cap dropped contacts / rows, PGS sweeps run, substeps."""
+    constraint rows, contacts kept; substeps where the contact cap dropped contacts, solver
+    iterations (Newton, or sweeps in study mode 1), substeps, physics warnings, and the
+    histogram of Newton iterations per substep ([63] = the iteration cap)."""
     found = np.zeros(STAT_HIST, np.int64)
-    rowreq = np.zeros(STAT_HIST, np.int64)
-    rows = np.zeros(64 + 2, np.int64)
+    rows = np.zeros(STAT_HIST, np.int64)
     cons = np.zeros(24 + 2, np.int64)
     misc = np.zeros(4, np.int64)
-    lib().ref_stats_get(found, rowreq, rows, cons, misc)
-    pdas = np.zeros(64, np.int64)
-    lib().ref_pdas_hist_get(pdas)
-    return dict(found=found, rowreq=rowreq, rows=rows, cons=cons, contact_cap_substeps=int(misc[0]),
-                row_cap_substeps=int(misc[1]), sweeps=int(misc[2]), substeps=int(misc[3]), pdas=pdas)
+    lib().ref_stats_get(found, rows, cons, misc)
+    newton = np.zeros(64, np.int64)
+    lib().ref_newton_hist_get(newton)
+    return dict(found=found, rows=rows, cons=cons, contact_cap_substeps=int(misc[0]), iterations=int(misc[1]),
+                substeps=int(misc[2]), warnings=int(misc[3]), newton=newton)
 
 
 def lib():
@@ -134,9 +137,11 @@ class OracleEnv:
 
     NV, NU, NACTION = 140, 44, 45
 
-    def __init__(self, model_desc, song_tables, cfg, n_envs: int, counting: bool = False, seed: int = 0):
+    def __init__(self, model_desc, song_tables, cfg, n_envs: int, counting: bool = False, seed: int = 0,
+                 env_offset: int = 0):
         """``counting``: run on the FLOP-counting build (bitwise the same results).
-        ``seed``: key of the randomize_hand_positions draws (as ps_create's)."""
+        ``seed``: key of the randomize_hand_positions draws (as ps_create's); ``env_offset``: the
+        global id of env 0 (as ps_set_env_offset)."""
         self._L = flops_lib() if counting else lib()
         from importlib import import_module
         abi = import_module("diffusion-piano_amd.abi")
@@ -155,6 +160,7 @@ class OracleEnv:
         self._h = self._L.ref_create(C.addressof(model_desc), C.addressof(sd), C.addressof(cfg), n_envs)
         self.obs_dim = self._L.ref_obs_dim(self._h)
         self._L.ref_set_seed(self._h, seed)
+        self._L.ref_set_env_offset(self._h, env_offset)
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -180,6 +186,12 @@ class OracleEnv:
         else:
             self._L.ref_step(self._h, a, obs, rew, disc, st)
         return obs, rew, disc, st
+
+    def warnings(self):
+        """[n, 3] int32: mj_checkPos / mj_checkVel / mj_checkAcc resets of each env since create."""
+        out = np.zeros((self.n, 3), np.int32)
+        self._L.ref_warnings(self._h, out)
+        return out
 
     def get_state(self):
         n = self.n

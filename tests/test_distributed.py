@@ -52,7 +52,15 @@ def _worker(rank, world, port, q):
         er.update(ids, torch.full((shard.count,), 2, dtype=torch.uint8))
         s, n, _, ne = er.gather()
         t = sh.max_over_ranks(1.0 + rank)
-        q.put((rank, s, n, ne, t))
+        # per-env float32 returns, uneven shards: 7 envs over 2 ranks (4 + 3)
+        odd = sh.shard_envs(7, rank, world)
+        er2 = sh.EpisodeReturns(odd.count, "cpu")
+        er2.update(torch.arange(odd.start, odd.stop, dtype=torch.float32) * 0.5,
+                   torch.full((odd.count,), 1, dtype=torch.uint8))
+        er2.update(torch.ones(odd.count), torch.tensor([2 if (odd.start + i) % 2 == 0 else 1
+                                                      for i in range(odd.count)], dtype=torch.uint8))
+        per_env = sh.gather_episode_returns(er2, odd, 7)
+        q.put((rank, s, n, ne, t, per_env.dtype == torch.float32, per_env.tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -68,8 +76,14 @@ def test_gloo_world2_gather_and_max():
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = sorted(q.get(timeout=5) for _ in range(2))
-    for rank, s, n, ne, t in res:
+    import math
+    for rank, s, n, ne, t, is_f32, per_env in res:
         assert s == pytest.approx(sum(range(8))) and n == 8 and ne == 8 and t == 2.0
+        # every rank holds all 7 envs in global order: even ids finished with 0.5 g + 1, odd ones
+        # have not finished an episode (NaN)
+        assert is_f32 and len(per_env) == 7
+        for g, v in enumerate(per_env):
+            assert (v == pytest.approx(0.5 * g + 1.0)) if g % 2 == 0 else math.isnan(v)
 
 
 # ------------------------------------------------------------------ bench.py rank logic

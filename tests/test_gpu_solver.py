@@ -1,9 +1,9 @@
-"""The exact constraint solve on the GPU against the oracle's, the round-1 PGS solver kept as an
-option, the solver / cap counters, and bitwise repeatability of contacts sharing a key.
+"""The Newton constraint solve on the GPU against the oracle's (friction-loss rows, uncapped
+rows, hands coupled through hand-hand contacts), the solver counters, and bitwise repeatability
+of contacts sharing a key.
 
 Tolerances (fp32 kernel vs fp64 oracle, same state and action, one control step): qpos
-median < 1e-6, p99 < 1e-4 (tighter than test_gpu_parity's bounds, which date from the
-truncated PGS solve)."""
+median < 1e-6, p99 < 1e-4."""
 import numpy as np
 import pytest
 
@@ -52,17 +52,10 @@ def test_exact_solver_teacher_forced_bench_song(dp, ref):
     assert np.median(e) < 1e-6 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
 
 
-def test_round1_pgs_solver_option(dp, ref):
-    """constraint_solver="pgs" keeps round 1's truncated solve, GPU = oracle."""
-    md, g, o = _pair(dp, ref, "twinkle", 32, constraint_solver="pgs")
-    assert g.task_cfg.solver == 0 and g.task_cfg.pgs_iterations == 20
-    e = _teacher_forced(md, g, o, 6, np.random.RandomState(3))
-    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 5e-4, (np.median(e), np.percentile(e, 99), e.max())
-
-
 def test_solver_stats_and_caps(dp):
-    """Counters of the bench workload: the exact solve needs ~1-2 linear solves per substep; the
-    contact cap (~1e-6 of the substeps) and the row cap (~2e-5) almost never bind."""
+    """Counters of the bench workload: Newton iterations per substep (~4-5: the oracle's mean
+    from a cold start is 4.7), never the iteration cap, no non-positive pivot, the contact cap
+    (~1e-6 of the substeps) almost never binding; ~40% of the substeps couple the hands."""
     N = 4096
     g = dp.BatchedPianoEnv(N, song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True), device="cuda:0")
     g.reset()
@@ -72,12 +65,72 @@ def test_solver_stats_and_caps(dp):
         g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
         st.append(g.solver_stats().cpu().numpy())
     st = np.stack(st)
-    solves = st[..., 0] / 10.0
-    assert 0.5 < solves.mean() < 3.0, solves.mean()
+    it = st[..., 0] / 10.0
     subs = st[..., 0].size * 10
+    print(f"Newton iterations/substep {it.mean():.2f}, cap {st[..., 2].sum()}, coupled {st[..., 4].sum() / subs:.3f}, "
+          f"bad pivots {st[..., 5].sum()}, max rows {st[..., 3].max()}")
+    assert 1.0 < it.mean() < 10.0, it.mean()
     assert st[..., 1].sum() <= 1e-4 * subs  # narrow phase found >= max_contacts (20) contacts
-    assert st[..., 2].sum() <= 1e-3 * subs  # coupled rows dropped past PS_MAX_ROWS
+    assert st[..., 2].sum() <= 1e-4 * subs  # Newton iteration cap
+    assert st[..., 5].sum() == 0            # non-positive pivots
+    assert 0.1 < st[..., 4].sum() / subs < 0.9
     assert st[..., 3].max() <= 96
+
+
+def _replay(dp, ref, select, steps=14, N=2048, seed=7):
+    """Roll N GPU envs; replay on the oracle the env-steps `select(stats, state)` picks."""
+    md, g, _ = _pair(dp, ref, "crossing_field", N)
+    lo, hi = dp_action_spec(md)
+    rng = np.random.RandomState(seed)
+    g.reset()
+    states, acts, outs = [], [], []
+    for _ in range(steps):
+        s0 = {k: v.cpu().numpy() for k, v in g.get_state().items()}
+        a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
+        g.step(torch.from_numpy(a).cuda())
+        pick = np.nonzero(select(g.solver_stats().cpu().numpy()) & (s0["last"] == 0))[0][:64]
+        if len(pick):
+            q1 = g.get_state()["qpos"].cpu().numpy()
+            states.append({k: s0[k][pick] for k in KEYS})
+            acts.append(a[pick])
+            outs.append(q1[pick])
+    n = sum(len(x) for x in acts)
+    st = {k: np.concatenate([s[k] for s in states]) for k in KEYS} if n else None
+    if not n:
+        return n, None
+    seq = song(dp, "crossing_field")
+    _, sttab, tc = dp.compile_task(seq, dp.TaskConfig(trim_silence=True), canonical_actions=False)
+    o = ref.OracleEnv(md, sttab, tc, n)
+    o.set_state(st)
+    o.step(np.concatenate(acts))
+    return n, np.abs(np.concatenate(outs) - o.get_state()["qpos"]).max(axis=1)
+
+
+def test_newton_heavy_states(dp, ref):
+    """States with 10+ contacts in a substep (40+ contact rows besides the 52 friction-loss rows:
+    round 2 dropped rows past 64) replayed on the oracle."""
+    n, e = _replay(dp, ref, lambda st: st[:, 3] > 40)
+    assert n >= 4, f"only {n} heavy env-steps"
+    print(f"{n} heavy env-steps: qpos err median {np.median(e):.2e} p90 {np.percentile(e, 90):.2e} max {e.max():.2e}")
+    assert np.median(e) < 1e-5 and np.percentile(e, 90) < 1e-4, (np.median(e), np.percentile(e, 90), e.max())
+
+
+def test_newton_coupled_hands(dp, ref):
+    """Env-steps whose every substep coupled the hands (hand-hand contact: the C-block
+    elimination after both hands' independent pivots) replayed on the oracle."""
+    n, e = _replay(dp, ref, lambda st: st[:, 4] >= 10)
+    assert n >= 16, f"only {n} coupled env-steps"
+    print(f"{n} coupled env-steps: qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}")
+    assert np.median(e) < 1e-6 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
+
+
+def test_newton_coupled_hands_full_block(dp, ref, monkeypatch):
+    """The same on the 28-column C block (taken when a hand has more than 16 C dofs; forced here
+    for every coupled substep by the test hook)."""
+    monkeypatch.setenv("PIANOSIM_DEBUG_FULL_COUPLED", "1")
+    n, e = _replay(dp, ref, lambda st: st[:, 4] >= 10, steps=8)
+    assert n >= 8, f"only {n} coupled env-steps"
+    assert np.median(e) < 1e-6 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
 
 
 def test_same_key_contacts_bitwise_repeatable(dp, ref):
@@ -112,37 +165,3 @@ def test_same_key_contacts_bitwise_repeatable(dp, ref):
         q = g.get_state()["qpos"]
         assert torch.equal(q, q[:1].expand_as(q))
         assert torch.equal(obs, obs[:1].expand_as(obs)) and torch.equal(rew, rew[:1].expand_as(rew))
-
-
-def test_exact_solver_large_free_sets(dp, ref):
-    """States whose coupled-row count passes 40 (above 32 rows the kernel solves on the
-    48/64-column principal pivot tableau with its lane state parked, dual_ppt) replayed on the
-    oracle: the same step to the tolerance of the 64-env bench-song test above, on the
-    heaviest states the workload produces."""
-    N = 2048
-    md, g, _ = _pair(dp, ref, "crossing_field", N)
-    lo, hi = dp_action_spec(md)
-    rng = np.random.RandomState(7)
-    g.reset()
-    states, acts, outs = [], [], []
-    for _ in range(14):
-        s0 = {k: v.cpu().numpy() for k, v in g.get_state().items()}
-        a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
-        g.step(torch.from_numpy(a).cuda())
-        heavy = np.nonzero((g.solver_stats().cpu().numpy()[:, 3] > 40) & (s0["last"] == 0))[0]
-        if len(heavy):
-            q1 = g.get_state()["qpos"].cpu().numpy()
-            states.append({k: s0[k][heavy] for k in KEYS})
-            acts.append(a[heavy])
-            outs.append(q1[heavy])
-    n = sum(len(x) for x in acts)
-    assert n >= 4, f"only {n} heavy env-steps"
-    st = {k: np.concatenate([s[k] for s in states]) for k in KEYS}
-    seq = song(dp, "crossing_field")
-    _, sttab, tc = dp.compile_task(seq, dp.TaskConfig(trim_silence=True), canonical_actions=False)
-    o = ref.OracleEnv(md, sttab, tc, n)
-    o.set_state(st)
-    o.step(np.concatenate(acts))
-    e = np.abs(np.concatenate(outs) - o.get_state()["qpos"]).max(axis=1)
-    print(f"{n} heavy env-steps: qpos err median {np.median(e):.2e} p90 {np.percentile(e, 90):.2e} max {e.max():.2e}")
-    assert np.median(e) < 1e-5 and np.percentile(e, 90) < 1e-4, (np.median(e), np.percentile(e, 90), e.max())

@@ -47,9 +47,10 @@ def test_authored_hand_matches_the_table(table, fresh):
 
 def test_every_row_has_a_source(table):
     for r in table["rows"]:
-        assert r["status"] in ("transcribed", "verifiable", "deviation"), r
+        assert r["status"] in ("transcribed", "verifiable", "deviation", "assumed"), r
         assert r["source"], r
         assert (r["status"] == "deviation") == r["source"].startswith("DEV"), r
+        assert (r["status"] == "assumed") == r["source"].startswith("ASSUMED"), r
     assert table["counts"] == {"bodies": 25, "dofs": 26, "actuators": 22, "tendons": 4,
                                "colliders": 20, "sites": 5}
 
@@ -84,7 +85,15 @@ def test_reference_side_rows(table):
 def test_deviations_are_the_documented_ones(table):
     dev = [r for r in table["rows"] if r["status"] == "deviation"]
     kinds = {r["quantity"].split()[0] for r in dev}
-    assert kinds == {"joint", "collider"}  # frictionloss not modelled; capsule colliders
-    assert all(r["value"] == 0.0 for r in dev if r["quantity"].startswith("joint"))
+    assert kinds == {"collider"}  # the capsule colliders (frictionloss is modelled since round 3)
     design = (ROOT / "DESIGN.md").read_text()
     assert "hand_provenance.json" in design
+
+
+def test_frictionloss_is_modelled(table):
+    """the 26 joint frictionloss rows are transcribed (modelled), no longer
+    deviations; the only deviations left are the capsule colliders."""
+    fl = [r for r in table["rows"] if r["quantity"].endswith(" frictionloss")]
+    assert len(fl) == 26 and all(r["status"] == "transcribed" and r["value"] == 0.01 for r in fl)
+    dev = [r for r in table["rows"] if r["status"] == "deviation"]
+    assert len(dev) == 20 and all(r["quantity"].startswith("collider ") for r in dev)

@@ -105,7 +105,7 @@ def test_cylinder_collider_becomes_capsule_and_visuals_are_skipped(mj, base_xml)
     spec = mj.load_hand(xml)
     assert spec.geoms[0].radius == 0.035 and spec.geoms[0].halflen == 0.06
     xml = _edit(base_xml, '<geom class="plastic_visual" mesh="forearm" />',
-                '<geom class="plastic_visual" mesh="forearm" contype="1" />')
+                '<geom class="plastic_visual" mesh="forearm" contype="1" conaffinity="1" />')
     with pytest.raises(ValueError, match="unknown mesh 'forearm'"):  # a colliding mesh needs its asset
         mj.load_hand(xml)
 
@@ -143,3 +143,86 @@ def test_errors(mj, base_xml):
         mj.load_hand(_edit(base_xml, 'name="rh_WRJ2"', 'name="rh_WRJ2" type="ball"'))
     with pytest.raises(ValueError, match="unknown joint"):
         mj.load_hand(_edit(base_xml, 'joint="rh_FFJ2" coef', 'joint="rh_XXJ2" coef'))
+
+
+def test_frictionloss_and_contact_params_are_read(dp, mj, base_xml):
+    """joint frictionloss (class default and per joint) reaches dof_frictionloss, the forearm
+    slides inherit the root class's value; the colliders' solref / solimp / friction become the
+    hand contact parameters, and MuJoCo's defaults fill what the XML leaves out."""
+    spec = mj.load_hand(base_xml)
+    assert all(d.frictionloss == 0.01 for d in spec.dofs)
+    md = dp.model.build_model(hand=spec)
+    np.testing.assert_array_equal(np.ctypeslib.as_array(md.dof_frictionloss), 0.01)
+    np.testing.assert_allclose(md.hand_contact.solref, (0.005, 1.0))
+    xml = _edit(base_xml, 'name="rh_WRJ2"', 'name="rh_WRJ2" frictionloss="0.2"')
+    spec = mj.load_hand(xml)
+    assert {d.name: d.frictionloss for d in spec.dofs}["WRJ2"] == 0.2
+    xml = _edit(base_xml, 'frictionloss="0.01"', 'frictionloss="0.03"')
+    assert all(d.frictionloss == 0.03 for d in mj.load_hand(xml).dofs)
+    # no solref/solimp on the colliders: MuJoCo's defaults
+    xml = _edit(base_xml, 'solref="0.005 1.0" solimp="0.5 0.99 0.0001 0.5 2.0" ', '')
+    sr, si, fr = mj.load_hand(xml).contact
+    assert sr == mj.MJ_SOLREF and si == mj.MJ_SOLIMP and fr == 1.0
+    # partial solimp: the rest from the defaults
+    xml = _edit(base_xml, 'solimp="0.5 0.99 0.0001 0.5 2.0"', 'solimp="0.5 0.99 0.0001"')
+    assert mj.load_hand(xml).contact[1] == (0.5, 0.99, 0.0001, 0.5, 2.0)
+
+
+@pytest.mark.parametrize("old,new,match", [
+    # joints
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" margin="0.01"', "margin"),
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" solreflimit="0.01 1"', "solreflimit"),
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" solimpfriction="0.8 0.9 0.001"', "solimpfriction"),
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" pos="0 0 0.01"', "pos"),
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" ref="0.1"', "ref"),
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" actuatorfrclimited="true"', "actuatorfrclimited"),
+    ('name="rh_WRJ2"', 'name="rh_WRJ2" polycoef="0 1 0 0 0"', "polycoef"),
+    # colliders (through the class default: every collider of the class)
+    ('group="3"', 'group="3" condim="4"', "condim"),
+    ('group="3"', 'group="3" margin="0.001"', "margin"),
+    ('group="3"', 'group="3" gap="0.001"', "gap"),
+    ('group="3"', 'group="3" contype="2"', "contype"),
+    ('group="3"', 'group="3" conaffinity="3"', "conaffinity"),
+    ('group="3"', 'group="3" priority="1"', "priority"),
+    ('group="3"', 'group="3" solmix="0.5"', "solmix"),
+    # one collider with its own contact parameters: two sets
+    ('<geom class="plastic_collision" size="0.035 0.06"', '<geom class="plastic_collision" solref="0.01 1" '
+     'size="0.035 0.06"', "different solref"),
+    # actuators
+    ('<position class="right_hand" kp', '<position class="right_hand" kv="0.1" kp', "kv"),
+    ('<position class="right_hand" kp', '<position class="right_hand" gear="2" kp', "gear"),
+    ('<position class="right_hand" kp', '<position class="right_hand" dampratio="1" kp', "dampratio"),
+    # tendons
+    ('<fixed name="rh_T0"', '<fixed name="rh_T0" stiffness="1"', "stiffness"),
+    ('<fixed name="rh_T0"', '<fixed name="rh_T0" frictionloss="0.1"', "frictionloss"),
+    ('<fixed name="rh_T0"', '<fixed name="rh_T0" range="0 1"', "tendon limits"),
+    # bodies
+    ('name="rh_palm"', 'name="rh_palm" gravcomp="1"', "gravcomp"),
+    ('name="rh_palm"', 'name="rh_palm" mocap="true"', "mocap"),
+    # model-level options and elements
+    ('<compiler ', '<option integrator="implicitfast" /><compiler ', "integrator"),
+    ('<compiler ', '<option cone="elliptic" /><compiler ', "cone"),
+    ('<compiler ', '<option impratio="10" /><compiler ', "impratio"),
+    ('<compiler ', '<option noslip_iterations="3" /><compiler ', "noslip_iterations"),
+    ('<compiler ', '<option gravity="0 0 -1" /><compiler ', "gravity"),
+    ('<compiler ', '<option><flag warmstart="disable" /></option><compiler ', "flag"),
+    ('<compiler ', '<equality /><compiler ', "equality"),
+    ('angle="radian"', 'angle="radian" boundmass="0.001"', "boundmass"),
+    ('angle="radian"', 'angle="radian" inertiafromgeom="true"', "inertiafromgeom"),
+    ('<exclude ', '<pair geom1="a" geom2="b" /><exclude ', "pair"),
+    ('<fixed name="rh_T0"', '<spatial name="s" /><fixed name="rh_T0"', "spatial"),
+    ('<inertial ', '<freejoint /><inertial ', "freejoint"),
+])
+def test_unmodelled_physics_is_rejected(mj, base_xml, old, new, match):
+    """Fail closed: any physics attribute or element the kernel does not
+    simulate raises ValueError instead of being dropped."""
+    with pytest.raises(ValueError, match=match):
+        mj.load_hand(_edit(base_xml, old, new))
+
+
+def test_harmless_attributes_are_accepted(mj, base_xml):
+    """Names, visuals and solver-effort options do not change the simulated hand."""
+    xml = _edit(base_xml, '<compiler ', '<option timestep="0.002" iterations="50" tolerance="1e-10" '
+                'solver="Newton" integrator="Euler" cone="pyramidal" /><compiler ')
+    xml = _edit(xml, 'group="3"', 'group="3" rgba="1 0 0 1" condim="3" margin="0" priority="0"')
+    mj.load_hand(xml)

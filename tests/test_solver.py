@@ -1,10 +1,10 @@
 """The constraint solve and the caps, on the oracle (CPU).
 
-* The specification's exact dual solve (warm-up PGS + block principal pivoting) equals PGS run
-  to convergence from a cold start - an independent method for the same unique solution (the
-  one MuJoCo's solvers converge to) - on random-action states of the benchmark song.
-* Round 1's truncated solver (20 cold-start PGS sweeps) is measurably NOT that solution.
-* The contact cap never binds in a random-action rollout, the coupled-row cap only rarely.
+* The specification's primal Newton solve (MuJoCo's default solver, with friction-loss rows and
+  no row cap) equals the dual problem solved by projected Gauss-Seidel run to convergence from a
+  cold start (friction-loss forces boxed to +-frictionloss) - an independent method for the same
+  unique solution - on random-action states of the benchmark song.
+* Newton converges in every substep; the contact cap never binds; rows are uncapped.
 * randomize_hand_positions: the counter-based U(-0.05, 0.05) draws and the hand shift.
 """
 import numpy as np
@@ -51,51 +51,49 @@ def test_exact_solve_is_the_converged_solution(dp, ref):
     assert max(gaps) < 1e-9, gaps
 
 
-def test_round1_pgs20_is_not_converged(dp, ref):
-    """The study behind the solver change (profiles/r02_solver_study.json): 20 cold-start PGS
-    sweeps leave a one-control-step qpos gap far above the fp32 parity tolerance."""
-    md, st, tc, env = _env(dp, ref, 16)
-    _, _, tc_pgs, env_pgs = _env(dp, ref, 16, constraint_solver="pgs")
-    assert tc.solver == 1 and tc_pgs.solver == 0 and tc_pgs.pgs_iterations == 20
-    rng = np.random.RandomState(3)
-    lo, hi = _rollout(ref, env, md, 12, rng)
-    s = env.get_state()
-    env_pgs.set_state(s)
-    a = rng.uniform(lo, hi, (16, 45)).astype(np.float32)
-    env.step(a)
-    env_pgs.step(a)
-    gap = np.abs(env.get_state()["qpos"] - env_pgs.get_state()["qpos"]).max()
-    assert gap > 1e-4, gap
+def test_pgs_solver_is_retired(dp):
+    with pytest.raises(ValueError, match="retired"):
+        dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(constraint_solver="pgs"))
+    _, _, tc = dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(constraint_solver="exact"))
+    assert tc.solver == 1 and tc.solver_iterations == 0
 
 
-def test_caps_rarely_bind_in_random_rollouts(dp, ref):
-    """The contact cap (20) never binds; the coupled-row cap (64 = one row per lane) binds in
-    ~1e-4 of the substeps under uniform random actions, where position targets at the joint
-    ranges push many hand joints past their limits at once (profiles/r02_solver_study.json
-    has the rates over longer rollouts)."""
+def test_newton_converges_and_no_row_cap(dp, ref):
+    """The Newton solve converges in every substep of a random-action rollout (never at its
+    iteration cap); the contact cap (20) does not bind; constraint rows are not capped - the
+    52 friction-loss rows alone are most of round 2's 64-row cap; with key limits and contacts the
+    substeps carry up to ~200 rows."""
     md, st, tc, env = _env(dp, ref, 16)
     ref.stats_reset()
     _rollout(ref, env, md, 40, np.random.RandomState(5))
     s = ref.stats()
     assert s["substeps"] == 16 * 40 * 10
     assert s["contact_cap_substeps"] == 0
-    assert s["row_cap_substeps"] <= 2e-3 * s["substeps"]
-    assert s["pdas"][63] == 0  # the exact solve never hit its iteration cap
+    assert s["newton"][63] == 0
+    assert s["newton"][:63].sum() == s["substeps"]
+    assert s["iterations"] / s["substeps"] < 8
+    rows = np.nonzero(s["rows"])[0]
+    assert rows.min() >= 52 and rows.max() > 150  # 52 friction rows always, + limits + contacts
     found = s["found"]
     assert np.nonzero(found)[0].max() < tc.max_contacts
+    assert s["warnings"] == 0
 
 
-def test_exact_solver_needs_no_sweeps(dp, ref):
-    """The warm-up only picks the start set: with 0 or 8 sweeps the solution is the same."""
-    md, st, tc0, env0 = _env(dp, ref, 8, pgs_iterations=0)
-    _, _, tc8, env8 = _env(dp, ref, 8, pgs_iterations=8)
-    rng = np.random.RandomState(9)
-    lo, hi = _rollout(ref, env8, md, 10, rng)
-    env0.set_state(env8.get_state())
-    a = rng.uniform(lo, hi, (8, 45)).astype(np.float32)
+def test_frictionloss_rows_act(dp, ref):
+    """With the Menagerie frictionloss the dynamics differ measurably from frictionloss 0 (the
+    rows are in the solve), and a zero frictionloss model equals the solve without those rows."""
+    md, st, tc, env = _env(dp, ref, 4)
+    md0, _, _ = dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True), canonical_actions=False)
+    np.ctypeslib.as_array(md0.dof_frictionloss)[:] = 0.0
+    env0 = ref.OracleEnv(md0, st, tc, 4)
+    rng = np.random.RandomState(2)
+    lo, hi = _rollout(ref, env, md, 6, rng)
+    env0.set_state(env.get_state())
+    a = rng.uniform(lo, hi, (4, 45)).astype(np.float32)
+    env.step(a)
     env0.step(a)
-    env8.step(a)
-    assert np.abs(env0.get_state()["qpos"] - env8.get_state()["qpos"]).max() < 1e-9
+    gap = np.abs(env.get_state()["qvel"] - env0.get_state()["qvel"]).max()
+    assert gap > 1e-3, gap
 
 
 # ------------------------------------------------------------------ randomize_hand_positions
@@ -106,6 +104,22 @@ def test_hand_offset_draws(ref):
     assert ref.hand_offset_draw(7, 3, 5) == d[3, 5]  # a pure function of (seed, env, episode)
     assert ref.hand_offset_draw(8, 3, 5) != d[3, 5]
     assert len(np.unique(d)) >= d.size - 4  # 24-bit draws: a few birthday collisions at most
+
+
+def test_hand_offsets_keyed_by_global_env(dp, ref):
+    """draws keyed by global env id - env g gets the same hand offset whether the job
+    runs on one handle (world 1) or is sharded over two (env_offset = shard start)."""
+    seq = song(dp, "twinkle")
+    md, st, tc = dp.compile_task(seq, dp.TaskConfig(randomize_hand_positions=True), canonical_actions=False)
+    whole = ref.OracleEnv(md, st, tc, 6, seed=5)
+    halves = [ref.OracleEnv(md, st, tc, 3, seed=5, env_offset=off) for off in (0, 3)]
+    for e in (whole, *halves):
+        e.reset()
+        e.reset()  # second episode
+    dy = whole.hand_offset()[0]
+    np.testing.assert_array_equal(np.concatenate([h.hand_offset()[0] for h in halves]), dy)
+    np.testing.assert_array_equal(dy.astype(np.float32),
+                                  np.array([ref.hand_offset_draw(5, g, 1) for g in range(6)], np.float32))
 
 
 def test_randomized_reset_shifts_both_hands(dp, ref):

@@ -71,8 +71,10 @@ def table():
                 f"{MJX} <default class='{'wrist' if d.name.startswith('WR') else 'right_hand'}'><joint damping>",
                 "transcribed")
         add(f"joint {d.name} armature", d.armature, f"{MJX} <default class='right_hand'><joint armature>", "transcribed")
-        add(f"joint {d.name} frictionloss", 0.0,
-            f"DEV: {MJX} class right_hand sets frictionloss 0.01; not modelled (no frictionloss rows)", "deviation")
+        add(f"joint {d.name} frictionloss", d.frictionloss,
+            f"{MJX} <default class='right_hand'><joint frictionloss> (the forearm slides inherit the root "
+            "childclass, shadow_hand.py:272-311); one friction-loss row per dof in every substep's solve",
+            "transcribed")
     dof_names = [d.name for d in hand.dofs]
     for a, (kind, target, kp, cr, fr) in enumerate(hand.acts):
         tname = dof_names[target] if kind == 0 else f"tendon {target}"
@@ -101,12 +103,31 @@ def table():
             "verifiable")
     for a, b in hand.excludes:
         add("contact exclude", [hand.bodies[a].name, hand.bodies[b].name], f"{MJX} <contact><exclude>", "transcribed")
+    sr, si, fr = hand.contact
+    src = f"{MJX} <default class='plastic'>/<geom> contact attributes of the collision geoms"
+    add("collider solref", list(sr), src, "transcribed")
+    add("collider solimp", list(si), src, "transcribed")
+    add("collider friction (sliding)", fr, src, "transcribed")
+    assumed = ("ASSUMED: MuJoCo's default (the Menagerie XML is not in this container); mjcf.load_hand raises "
+               "on any other value in a user XML")
+    add("collider condim", 3, assumed, "assumed")
+    add("collider margin / gap", [0.0, 0.0], assumed, "assumed")
+    add("collider contype / conaffinity", [1, 1], assumed, "assumed")
+    add("joint solreffriction", [0.02, 1.0], assumed, "assumed")
+    add("joint solimpfriction", [0.9, 0.95, 0.001, 0.5, 2.0], assumed, "assumed")
+    add("joint solreflimit", [0.02, 1.0], assumed, "assumed")
+    add("joint solimplimit", [0.9, 0.95, 0.001, 0.5, 2.0], assumed, "assumed")
+    add("option integrator", "Euler", assumed + " (dm_control composer physics; the reference sets none)", "assumed")
+    add("option cone", "pyramidal", assumed, "assumed")
+    add("option impratio", 1.0, assumed, "assumed")
+    add("option noslip_iterations", 0, assumed, "assumed")
     add("joints_pos order", [dof_names[i] for i in hand.obs_order],
         "RP hands/base.py:76-78 + shadow_hand_test.py:101-106 (Menagerie joints, forearm joints appended)", "verifiable")
     out = {"hand": "Shadow Hand E3M5 (right; the left hand is its mirror image, model.build_model)",
            "sources": {"MJX": MJX + " at Menagerie 1afc8be (scripts/install_deps.sh:81); absent from this container",
                        "RP": "reference files under /root/reference/robopianist",
-                       "DEV": "deviation, DESIGN.md section 3"},
+                       "DEV": "deviation, DESIGN.md section 3",
+                       "ASSUMED": "a MuJoCo default the absent XML may override; the loader fails closed on it"},
            "counts": {"bodies": len(hand.bodies), "dofs": len(hand.dofs), "actuators": len(hand.acts),
                       "tendons": len(hand.tendons), "colliders": len(hand.geoms), "sites": len(hand.sites)},
            "rows": rows}

@@ -23,18 +23,19 @@ for i in range(10):
 st = np.stack(stats)  # [10, N, 4]
 out = np.zeros((N, 28), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
-names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
-         3: "factor", 4: "solve_smooth",
-         12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T", 15: "cons:finish",
-         16: "pgs:build A", 17: "pgs:sweeps", 18: "ex:rest", 19: "ex:start set", 23: "ex:tableau", 20: "ex:factor+solve", 21: "ex:w+check", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
+names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest",
+         11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs", 18: "newton:prep", 3: "factor", 4: "solve_smooth",
+         12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
+         8: "nt:J'f", 6: "integrate", 5: "final+task"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
 for i, n in names.items():
     v = out[:, i].astype(np.float64)
     print(f"{n:14s} {v.mean()/10:12.0f} cycles/env-step  {100*v.sum()/tot.sum():5.1f}%")
 print(f"total {tot.mean()/10:.0f} cycles/env-step per wave; mean rows/substep {out[:,9].mean()/100:.1f} mean contacts {out[:,10].mean()/100:.2f}")
 solves = st[..., 0] / 10.0
-print(f"exact solve: linear solves per substep mean {solves.mean():.3f}, max over env-steps {st[..., 0].max()} per step; "
-      f"contact-cap substeps {int(st[..., 1].sum())}, row-cap substeps {int(st[..., 2].sum())}, max rows {int(st[..., 3].max())}")
+print(f"Newton: iterations per substep mean {solves.mean():.3f}, max over env-steps {st[..., 0].max()} per step; "
+      f"contact-cap substeps {int(st[..., 1].sum())}, iteration-cap substeps {int(st[..., 2].sum())}, "
+      f"max contact rows {int(st[..., 3].max())}, coupled substeps {st[..., 4].sum() / (10 * st[..., 4].size):.3f}")
 # the per-env spread sets the tail of a launch (4096 envs = 2 rounds of 2048 slots)
 per = tot / 10
 q = np.percentile(per, [50, 90, 99, 100])
@@ -47,7 +48,7 @@ for i, n in names.items():
 # the slowest envs, phase by phase (what sets a launch's tail at one round of workgroups)
 worst = np.argsort(per)[-3:][::-1]
 print("slowest envs (cycles/env-step):", ", ".join(f"{per[w]:.0f}" for w in worst),
-      "| solves per step:", ", ".join(str(int(st[:, w, 0].sum() / 10)) for w in worst),
-      "| max rows:", ", ".join(str(int(st[:, w, 3].max())) for w in worst))
+      "| Newton iterations per step:", ", ".join(str(int(st[:, w, 0].sum() / 10)) for w in worst),
+      "| max contact rows:", ", ".join(str(int(st[:, w, 3].max())) for w in worst))
 for i, n in names.items():
     print(f"  worst {n:14s} " + " ".join(f"{out[w, i] / 10:10.0f}" for w in worst))

@@ -67,7 +67,8 @@ def main():
 
     seq, task = load_song(dp, args.song)
     shard = sharding.shard_envs(args.envs * world, rank, world)
-    env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=shard.start)
+    env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
+                             env_offset=shard.start)
     torch.manual_seed(0)
     agent = ppo.PPOAgent(env.obs_dim, 45, lr=1e-4, gamma=0.99, epsilon=0.2, batch_size=args.batch,
                          ppo_epochs=args.epochs, checkpoint_dir="/tmp/ppo_bench_ckpt", use_wandb=False,
