@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
     p.add_argument("--song", default="crossing_field", choices=["twinkle", "crossing_field", "guren"])
+    p.add_argument("--hand", default="authored", choices=["authored", "hull"],
+                   help="authored: capsule colliders (primitive_fingertip_collisions=True); hull: palm boxes "
+                        "and convex-hull fingertips, the reference's default collider kinds (shadow_hand.py:95,144-152)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-envs", type=int, default=16)
     p.add_argument("--cpu-sample-steps", type=int, default=1000)
@@ -138,20 +141,24 @@ def _profile(name, sha=None):
     return d
 
 
-def pmc_traffic(n_envs, song, sha):
+def _pmc_match(d, n_envs, song, hand):
+    return d and d.get("envs") == n_envs and d.get("song", song) == song and d.get("hand", "authored") == hand
+
+
+def pmc_traffic(n_envs, song, sha, hand="authored"):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary of THIS build, else None."""
     d = _profile("pmc_latest.json", sha)
-    if d and d.get("envs") == n_envs and d.get("song", song) == song:
+    if _pmc_match(d, n_envs, song, hand):
         return d.get("hbm_bytes_per_launch")
     return None
 
 
-def issue_summary(n_envs, song, sha):
+def issue_summary(n_envs, song, sha, hand="authored"):
     """Where the wave time goes (the binding limit: latency, not HBM), from the committed SQ
     counter pass of THIS build (tools/collect_pmc.py): fractions of the waves' lifetime
     issuing / waiting."""
     d = _profile("pmc_latest.json", sha)
-    if d and d.get("envs") == n_envs and d.get("song", song) == song and "wave_issue_frac" in d:
+    if _pmc_match(d, n_envs, song, hand) and "wave_issue_frac" in d:
         return {k: d[k] for k in ("wave_issue_frac", "wave_wait_frac", "wave_issue_stall_frac", "valu_insts_per_env_step")}
     return None
 
@@ -265,6 +272,9 @@ def main():
     dp = importlib.import_module("diffusion-piano_amd")
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
     seq, task = load_song(dp, args.song)
+    if args.hand == "hull":
+        import dataclasses
+        task = dataclasses.replace(task, hand_xml=dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand()))
     shard = sharding.shard_envs(args.envs * world, rank, world)  # weak scaling: envs per GPU fixed
     env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
                              env_offset=shard.start)
@@ -289,7 +299,7 @@ def main():
         sha = lib_sha()
         bpe = bytes_per_env_step(env.obs_dim)
         achieved = bpe * N / (kernel_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(N, args.song, sha)
+        traffic = pmc_traffic(N, args.song, sha, args.hand)
         line = {
             "metric": METRIC,
             "value": value,
@@ -308,6 +318,8 @@ def main():
                                    f"per env-step, constraint forces by the primal Newton solve (friction loss, "
                                    f"uncapped rows)",
                        "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
+                       "hand": args.hand + (" (capsule colliders)" if args.hand == "authored" else
+                                            " (palm boxes + convex-hull fingertips, pianosim_kernel<true>)"),
                        "mean_return_logged": mean_ret, "episodes_finished": fin_n,
                        "per_env_returns_gathered": int(per_env.numel()),
                        "mean_last_episode_return": float(per_env_done.mean()) if per_env_done.numel() else None,
@@ -323,7 +335,7 @@ def main():
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
                          "kernel_ms_note": "HIP events around ps_step on the launch stream: order_kernel "
                                            "(counting sort, ~5 us) + pianosim_kernel",
-                         "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song, sha),
+                         "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song, sha, args.hand),
                          "profile_note": "traffic / wave_time: rocprofv3 PMC passes of this library build "
                                          "(profiles/pmc_latest.json lib_sha), null when none exists"},
             "valu_roofline": valu_roofline(args.song, N, kernel_ms),

@@ -324,9 +324,18 @@ class BatchedPianoEnv:
         _lib.check(_lib.load().ps_musical_metrics(self._h, ep.data_ptr(), cnt.data_ptr(), self.stream))
         return ep, cnt
 
+    def warnings(self):
+        """[N, 3] int32: each env's mj_checkPos / mj_checkVel / mj_checkAcc resets since create
+        (ps_warnings). MuJoCo resets the data of a diverged env and raises the warning that
+        dm_control turns into ``PhysicsError``; the kernel does the reset per env and counts."""
+        t = self._torch.empty(self.num_envs, abi.NWARN, device=self.device, dtype=self._torch.int32)
+        _lib.check(_lib.load().ps_warnings(self._h, t.data_ptr(), self.stream))
+        return t
+
     def solver_stats(self):
-        """[N, 4] int32 counters of each env's last step: exact-solve linear solves, substeps at
-        the contact cap, substeps that dropped rows past PS_MAX_ROWS, most rows requested."""
+        """[N, 6] int32 counters of each env's last step (PS_STAT_*): Newton iterations, substeps
+        at the contact cap, substeps at the Newton iteration cap, most contact rows, substeps with
+        the hands coupled, substeps with a non-positive Hessian pivot."""
         t = self._torch.empty(self.num_envs, abi.NSTATS, device=self.device, dtype=self._torch.int32)
         _lib.check(_lib.load().ps_solver_stats(self._h, t.data_ptr(), self.stream))
         return t
@@ -424,21 +433,56 @@ class VectorizedPianoEnv:
         return obs_d, rew.clone(), dones
 
 
-class Environment:
-    """Single-env dm_env facade (``composer_utils.Environment`` + ``CanonicalSpecWrapper``)."""
+class PhysicsError(RuntimeError):
+    """dm_control's ``control.PhysicsError``: the simulation diverged (MuJoCo's mj_checkPos /
+    mj_checkVel / mj_checkAcc warning: a NaN or |x| > 1e10 qpos, qvel or qacc)."""
 
-    def __init__(self, midi, task: Optional[TaskConfig] = None, device=None, seed: int = 0):
+
+_WARN_NAMES = ("mjWARN_BADQPOS", "mjWARN_BADQVEL", "mjWARN_BADQACC")
+
+
+class Environment:
+    """Single-env dm_env facade (``composer_utils.Environment`` + ``CanonicalSpecWrapper``).
+
+    Physics errors follow ``composer.Environment.step``: the kernel resets a diverged env's
+    physics and counts the warning (ps_warnings); with ``raise_exception_on_physics_error``
+    (composer's default, True) the step raises ``PhysicsError``, otherwise it logs the warning
+    and ends the episode with reward 0 and discount 0, and the next step resets."""
+
+    def __init__(self, midi, task: Optional[TaskConfig] = None, device=None, seed: int = 0,
+                 raise_exception_on_physics_error: bool = True):
         self._core = BatchedPianoEnv(1, midi, task, device=device, seed=seed)
+        self._raise = raise_exception_on_physics_error
+        self._warn = np.zeros(abi.NWARN, np.int64)
+        self._reset_next = False
+
+    def _obs(self, obs):
+        return {k: v[0].detach().cpu().numpy() for k, v in self._core.obs_dict(obs).items()}
 
     def reset(self) -> TimeStep:
+        self._reset_next = False
         obs = self._core.reset()
-        return TimeStep(StepType.FIRST, None, None,
-                        {k: v[0].detach().cpu().numpy() for k, v in self._core.obs_dict(obs).items()})
+        self._warn = self._core.warnings()[0].cpu().numpy().astype(np.int64)
+        return TimeStep(StepType.FIRST, None, None, self._obs(obs))
 
     def step(self, action) -> TimeStep:
+        if self._reset_next:
+            return self.reset()
         a = self._core._torch.as_tensor(np.asarray(action, np.float32).reshape(1, -1), device=self._core.device)
         obs, rew, disc, st = self._core.step(a)
-        o = {k: v[0].detach().cpu().numpy() for k, v in self._core.obs_dict(obs).items()}
+        o = self._obs(obs)
+        w = self._core.warnings()[0].cpu().numpy().astype(np.int64)
+        new = w - self._warn
+        self._warn = w
+        if new.any():
+            msg = "Physics state is invalid. Warning(s) raised: " + ", ".join(
+                n for n, c in zip(_WARN_NAMES, new) if c > 0)
+            if self._raise:
+                raise PhysicsError(msg)
+            import logging
+            logging.warning(msg)
+            self._reset_next = True
+            return TimeStep(StepType.LAST, 0.0, 0.0, o)
         t = StepType(int(st[0]))
         if t == StepType.FIRST:
             return TimeStep(t, None, None, o)

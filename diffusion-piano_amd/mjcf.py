@@ -575,7 +575,7 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
     hand = ET.SubElement(dflt, "default", {"class": "right_hand"})
     floss = spec.dofs[2].frictionloss
     ET.SubElement(hand, "joint", axis="1 0 0", damping="0.05", armature=repr(spec.dofs[2].armature),
-                  frictionloss=repr(floss))
+                  frictionloss=repr(float(floss)))
     ET.SubElement(hand, "position", forcerange="-1 1")
     wrist = ET.SubElement(hand, "default", {"class": "wrist"})
     ET.SubElement(wrist, "joint", damping="0.5")
@@ -620,7 +620,7 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
             if d.armature != spec.dofs[2].armature:
                 ja["armature"] = repr(d.armature)
             if d.frictionloss != floss:
-                ja["frictionloss"] = repr(d.frictionloss)
+                ja["frictionloss"] = repr(float(d.frictionloss))
             ET.SubElement(el, "joint", ja)
         ET.SubElement(el, "geom", {"class": "plastic_visual", "mesh": b.name})
         for g in spec.geoms:
@@ -667,3 +667,42 @@ def hand_to_mjcf(spec: M.HandSpec, prefix: str = "rh_") -> str:
         ET.SubElement(act, "position", aa)
     ET.indent(root)
     return ET.tostring(root, encoding="unicode")
+
+
+def capsule_points(radius, halflen, n_ring=8, n_lat=2) -> np.ndarray:
+    """Points on a capsule surface along z (a rounded fingertip shape for hull colliders)."""
+    pts = []
+    for z0, sgn in ((halflen, 1.0), (-halflen, -1.0)):
+        pts.append((0.0, 0.0, z0 + sgn * radius))
+        for j in range(n_lat + 1):
+            phi = (j / (n_lat + 1)) * np.pi / 2  # 0 at the equator
+            for i in range(n_ring):
+                t = 2 * np.pi * (i + 0.5 * (j % 2)) / n_ring
+                pts.append((radius * np.cos(phi) * np.cos(t), radius * np.cos(phi) * np.sin(t),
+                            z0 + sgn * radius * np.sin(phi)))
+    return np.asarray(pts)
+
+
+def box_hull_hand() -> M.HandSpec:
+    """The authored right hand with the reference's default collider kinds
+    (``primitive_fingertip_collisions=False``, shadow_hand.py:95,144-152: Menagerie palm boxes
+    and distal meshes): the two palm capsules and the little-finger metacarpal capsule become
+    boxes, every distal capsule a 58-point capsule-shaped convex hull (MuJoCo collides a mesh as
+    its hull). ``TaskConfig(hand_xml=hand_to_mjcf(box_hull_hand()))`` runs it through the MJCF
+    path; the step kernel's hull instantiation (pianosim_kernel<true>) then runs."""
+    hand = M.authored_hand()
+    geoms, xgeoms = [], []
+    names = [b.name for b in hand.bodies]
+    for g in hand.geoms:
+        bname = names[g.body]
+        if bname == "palm" or bname == "lfmetacarpal":
+            q = _quat_from_z(g.axis)
+            xgeoms.append(M.XGeom(g.body, "box", tuple(g.pos), tuple(q), (g.radius, g.radius * 0.8, g.halflen + g.radius)))
+        elif bname.endswith("distal"):
+            c, v = convex_hull_collider(capsule_points(g.radius, g.halflen))
+            R = M.quat_to_mat(_quat_from_z(g.axis))
+            pos = np.asarray(g.pos) + R @ c
+            xgeoms.append(M.XGeom(g.body, "hull", tuple(pos), tuple(_quat_from_z(g.axis)), verts=v))
+        else:
+            geoms.append(g)
+    return hand._replace(geoms=geoms, xgeoms=xgeoms)

@@ -350,6 +350,10 @@ class FusedStep:
         if B in self.bufs:
             return self.bufs[B]
         ag = self.agent
+        # keep the full-minibatch entry and ONE tail entry: with valid masks the tail size
+        # n % B changes every update, and each size's buffers would otherwise stay allocated
+        for k in [k for k in self.bufs if k != ag.batch_size]:
+            del self.bufs[k]
         f32 = dict(device=ag.device, dtype=torch.float32)
         sdim, adim = ag._S.shape[1], ag._A.shape[1]
         b = dict(S=torch.empty(B, sdim, **f32), A=torch.empty(B, adim, **f32), LP=torch.empty(B, **f32),
@@ -735,7 +739,10 @@ class PPOAgent:
         if self._wandb is not None:
             for rec in log.cpu().numpy():
                 self._wandb.log(dict(zip(LOG_KEYS, map(float, rec))))
-        stats = torch.stack([r.mean(), log[-1, 1]])
+        # the plateau signal: the mean normalised reward of the samples trained on (r holds 0
+        # at the dropped auto-reset rows)
+        r_mean = r.mean() if valid is None else r.reshape(-1)[_f32(valid, self.device).reshape(-1) != 0].mean()
+        stats = torch.stack([r_mean, log[-1, 1]])
         if self.distributed:  # one plateau decision for all replicas (else their lrs drift apart)
             torch.distributed.all_reduce(stats, group=self.process_group)
             stats /= torch.distributed.get_world_size(self.process_group)

@@ -94,3 +94,26 @@ def limit_equilibrium(md, p, side, applied=0.0):
         else:
             lo = mid
     return q_of(0.5 * (lo + hi))
+
+
+def frictionloss_qacc(md, xs, A, fl, v):
+    """One dof with a friction-loss row (MuJoCo: J = e_i, pos = 0, bound |f| <= frictionloss,
+    solreffriction / solimpfriction; every other row inactive). ``xs`` = the dof's acceleration
+    without the row (qacc_smooth: the same state with frictionloss 0), ``A`` = (M^-1)_ii = the
+    dof's invweight0 when the configuration is qpos0, ``v`` = the dof's velocity.
+    The soft row's reference acceleration is aref = -b v (b = 2 / (dmax timeconst); no
+    stiffness term at pos 0), R = (1 - imp) / imp * A, imp = imp(0) = d0. The minimiser of the
+    primal cost in the row's quadratic zone is f = -(xs - aref) / (A + R) ("creep": the
+    regularised stick); when |f| exceeds the bound the row saturates at f = -fl sign(xs - aref)
+    ("slip"). Returns (qacc of the dof = xs + A f, f, regime)."""
+    solref, solimp = list(md.friction_solref), list(md.friction_solimp)
+    dmax = min(max(solimp[1], 1e-4), 0.9999)
+    tc = max(solref[0], 2 * md.timestep)
+    aref = -(2.0 / (dmax * tc)) * v
+    imp = impedance(solimp, 0.0)
+    R = (1 - imp) / imp * A
+    f = -(xs - aref) / (A + R)
+    regime = "creep"
+    if abs(f) > fl:
+        f, regime = -fl * np.sign(xs - aref), "slip"
+    return xs + A * f, f, regime

@@ -36,38 +36,11 @@ def random_states(md, n, rng, vscale=0.5):
 
 
 def capsule_points(radius, halflen, n_ring=8, n_lat=2):
-    """Points on a capsule surface along z (a rounded fingertip shape for hull colliders)."""
-    pts = []
-    for z0, sgn in ((halflen, 1.0), (-halflen, -1.0)):
-        pts.append((0.0, 0.0, z0 + sgn * radius))
-        for j in range(n_lat + 1):
-            phi = (j / (n_lat + 1)) * np.pi / 2  # 0 at the equator
-            for i in range(n_ring):
-                t = 2 * np.pi * (i + 0.5 * (j % 2)) / n_ring
-                pts.append((radius * np.cos(phi) * np.cos(t), radius * np.cos(phi) * np.sin(t),
-                            z0 + sgn * radius * np.sin(phi)))
-    return np.asarray(pts)
+    """Points on a capsule surface along z (mjcf.capsule_points)."""
+    import importlib
+    return importlib.import_module("diffusion-piano_amd").mjcf.capsule_points(radius, halflen, n_ring, n_lat)
 
 
 def box_hull_hand(dp):
-    """The authored right hand with box and convex-hull colliders: the two palm capsules and the
-    little-finger metacarpal capsule become boxes, every distal capsule a 58-point capsule-shaped
-    hull (as the Menagerie hand's palm boxes and distal meshes)."""
-    M = dp.model
-    mj = dp.mjcf
-    hand = M.authored_hand()
-    geoms, xgeoms = [], []
-    names = [b.name for b in hand.bodies]
-    for g in hand.geoms:
-        bname = names[g.body]
-        if bname == "palm" or bname == "lfmetacarpal":
-            q = mj._quat_from_z(g.axis)
-            xgeoms.append(M.XGeom(g.body, "box", tuple(g.pos), tuple(q), (g.radius, g.radius * 0.8, g.halflen + g.radius)))
-        elif bname.endswith("distal"):
-            c, v = mj.convex_hull_collider(capsule_points(g.radius, g.halflen))
-            R = M.quat_to_mat(mj._quat_from_z(g.axis))
-            pos = np.asarray(g.pos) + R @ c
-            xgeoms.append(M.XGeom(g.body, "hull", tuple(pos), tuple(mj._quat_from_z(g.axis)), verts=v))
-        else:
-            geoms.append(g)
-    return hand._replace(geoms=geoms, xgeoms=xgeoms)
+    """The authored right hand with box and convex-hull colliders (mjcf.box_hull_hand)."""
+    return dp.mjcf.box_hull_hand()

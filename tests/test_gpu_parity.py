@@ -2,7 +2,8 @@
 
 Tolerances (fp32 kernel vs fp64 oracle, same inputs):
   * teacher-forced one physics substep : qpos |err| median < 1e-6, p99 < 5e-5
-  * teacher-forced one control step    : qpos |err| median < 1e-5, p99 < 5e-4
+  * teacher-forced one control step    : qpos |err| median < 1e-5, p99 < 1e-4 (BASELINE.md's
+    1e-4 parity target, per control step)
   * rewards                            : |err| p99 < 1e-3 (reward is O(1))
   * integer/bool outputs (step_type, discount, goal/fingering obs) : exact
 The maxima are not bounded tightly: a contact whose signed distance is within fp32
@@ -80,7 +81,7 @@ def test_teacher_forced_step(dp, ref, substep_only):
     if substep_only:
         assert med < 1e-6 and p99 < 5e-5, (med, p99, e.max())
     else:
-        assert med < 1e-5 and p99 < 5e-4, (med, p99, e.max())
+        assert med < 1e-5 and p99 < 1e-4, (med, p99, e.max())
 
 
 def test_teacher_forced_many_constraint_rows(dp, ref):
@@ -106,7 +107,7 @@ def test_teacher_forced_many_constraint_rows(dp, ref):
     g.step(torch.from_numpy(a).cuda())
     o.step(a)
     e = np.abs(_gstate(g)["qpos"] - o.get_state()["qpos"]).max(axis=1)
-    assert np.median(e) < 1e-6 and np.percentile(e, 90) < 5e-5, (np.median(e), np.percentile(e, 90), e.max())
+    assert np.median(e) < 1e-6 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
 
 
 @pytest.mark.parametrize("name,kw", [("twinkle", {}), ("crossing_field", dict(trim_silence=True)),

@@ -186,22 +186,34 @@ def test_rollout_trainer_on_env(ppo, reference_semantics, tmp_path):
     env.close()
 
 
+def _fused_agent(ppo, z, tmp_path, mfma, train_critic, batch):
+    ag = _agent(ppo, z, tmp_path, graphs=False)
+    ag.fused = True
+    if train_critic:
+        ag.critic.train()
+    ag._prepare(*batch)
+    ag._fused = ppo.FusedStep(ag)
+    ag._fused.mfma = mfma  # False: the hipBLASLt GEMMs + prl_lnrelu / head kernels (B > 512 path)
+    return ag
+
+
+@pytest.mark.parametrize("mfma", [True, False])
 @pytest.mark.parametrize("train_critic", [False, True])
-def test_fused_step_matches_autograd(ppo, tmp_path, train_critic):
-    """FusedStep (manual backward, libpianorl kernels between the GEMMs) against the torch
-    autograd step on the same weights and minibatch: logged losses and every gradient. With
-    the critic in train mode dropout is active on both sides with different masks, so there
-    only the actor side (no dropout) is compared."""
+def test_fused_step_matches_autograd(ppo, tmp_path, train_critic, mfma):
+    """FusedStep against the torch autograd step on the same weights and minibatch: logged
+    losses and every gradient, for both FusedStep paths (mfma: the one-kernel prl_mlp_step;
+    not: hipBLASLt GEMMs with libpianorl kernels between them). With the critic in train mode
+    dropout is active on both sides with different masks, so there only the actor side (no
+    dropout) is compared (test_fused_paths_agree_with_dropout compares the two fused paths)."""
     z = golden()
-    s, a, r, lp, ns, d = golden_batch(z, 0)
-    agents = []
-    for fused in (True, False):
-        ag = _agent(ppo, z, tmp_path, graphs=False)
-        ag.fused = fused
-        if train_critic:
-            ag.critic.train()
-        ag._prepare(s, a, r, lp, ns, d)
-        agents.append(ag)
+    batch = golden_batch(z, 0)
+    agents = [_fused_agent(ppo, z, tmp_path, mfma, train_critic, batch)]
+    ag = _agent(ppo, z, tmp_path, graphs=False)
+    ag.fused = False
+    if train_critic:
+        ag.critic.train()
+    ag._prepare(*batch)
+    agents.append(ag)
     idx = torch.randperm(96, generator=torch.Generator().manual_seed(3))[:32].cuda()
     rows = []
     for ag in agents:
@@ -218,8 +230,31 @@ def test_fused_step_matches_autograd(ppo, tmp_path, train_critic):
             np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * scale, err_msg=f"{net}.{k}")
 
 
-def test_fused_step_large_minibatch(ppo, tmp_path):
-    """B = 512 rows: the column sums run in 128-row chunks (partials + ordered final sum)."""
+def test_fused_paths_agree_with_dropout(ppo, tmp_path):
+    """The two FusedStep paths with the critic in train mode (dropout active): the matrix-core
+    kernel's dropout masks are prl_lnrelu_fwd's (same Philox keys: seed, minibatch counter,
+    layer, row, column), so the logged losses and every gradient agree tightly."""
+    z = golden()
+    batch = golden_batch(z, 0)
+    agents = [_fused_agent(ppo, z, tmp_path, m, True, batch) for m in (True, False)]
+    idx = torch.randperm(96, generator=torch.Generator().manual_seed(5))[:32].cuda()
+    rows = []
+    for ag in agents:
+        ag._forward_backward(idx, ag._log_row)
+        torch.cuda.synchronize()
+        rows.append(ag._log_row.cpu().numpy().copy())
+    np.testing.assert_allclose(rows[0], rows[1], rtol=2e-5, atol=2e-6)
+    for net in ("actor", "critic"):
+        for (k, p0), (_, p1) in zip(getattr(agents[0], net).named_parameters(), getattr(agents[1], net).named_parameters()):
+            g0, g1 = p0.grad.cpu().numpy(), p1.grad.cpu().numpy()
+            np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * max(np.abs(g1).max(), 1e-6), err_msg=f"{net}.{k}")
+
+
+@pytest.mark.parametrize("mfma", [True, False])
+def test_fused_step_large_minibatch(ppo, tmp_path, mfma):
+    """B = 512 rows against autograd, on both FusedStep paths: the matrix-core kernel at its
+    row limit, and the hipBLASLt path whose column sums run in 128-row chunks (partials +
+    ordered final sum)."""
     rng = np.random.RandomState(9)
     n, S = 1024, 64
     s = rng.rand(n, S).astype(np.float32)
@@ -234,6 +269,9 @@ def test_fused_step_large_minibatch(ppo, tmp_path):
                           graphs=False, fused=fused)
         ag.critic.eval()
         ag._prepare(s, a, r, lp, ns, d)
+        if fused:
+            ag._fused = ppo.FusedStep(ag)
+            ag._fused.mfma = mfma
         agents.append(ag)
     idx = torch.randperm(n, generator=torch.Generator().manual_seed(1))[:512].cuda()
     for ag in agents:

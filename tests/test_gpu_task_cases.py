@@ -8,7 +8,9 @@
   teacher-forced against the oracle step by step;
 * randomize_hand_positions: the GPU's draws are the oracle's bit for bit, and the shifted
   hands step alike;
-* VectorizedPianoEnv returns observations / rewards a driver may keep across steps.
+* VectorizedPianoEnv returns observations / rewards a driver may keep across steps;
+* diverged envs (NaN / |x| > 1e10 qpos or qvel): reset and flagged per env like MuJoCo's
+  mj_checkPos / mj_checkVel, the same as the oracle; Environment raises PhysicsError.
 """
 import numpy as np
 import pytest
@@ -89,20 +91,24 @@ def test_guren_at_4096_envs(dp, ref):
     s = g.get_state()
     assert torch.isfinite(s["qpos"]).all() and torch.isfinite(rew).all()
     assert torch.equal(s["qpos"][: N // 2], s["qpos"][N // 2:]) and torch.equal(obs[: N // 2], obs[N // 2:])
-    # 16 sampled envs, teacher-forced one step against the oracle
-    idx = np.arange(0, N, N // 16)
+    # 64 sampled envs, teacher-forced for 4 steps against the oracle (256 env-steps)
+    idx = np.arange(0, N, N // 64)
     o = ref.OracleEnv(md, st, tc, len(idx))
-    sg = _gs(g)
-    o.set_state({k: sg[k][idx] for k in KEYS})
-    a = lo + torch.rand(N, 45, device="cuda:0", generator=gen) * (hi - lo)
-    og, rg, _, tg = g.step(a)
-    oo, ro, _, to = o.step(a.cpu().numpy()[idx])
-    np.testing.assert_array_equal(tg.cpu().numpy()[idx], to)
-    eq = np.abs(g.get_state()["qpos"].cpu().numpy()[idx] - o.get_state()["qpos"]).max(axis=1)
-    assert np.median(eq) < 1e-5 and eq.max() < 1e-3, eq
-    assert np.abs(rg.cpu().numpy()[idx] - ro).max() < 1e-3
     lay = dp.obs_layout(tc)
-    np.testing.assert_array_equal(og.cpu().numpy()[idx][:, lay["fingering"]], oo[:, lay["fingering"]])
+    eqs, ers = [], []
+    for _ in range(4):
+        sg = _gs(g)
+        o.set_state({k: sg[k][idx] for k in KEYS})
+        a = lo + torch.rand(N, 45, device="cuda:0", generator=gen) * (hi - lo)
+        og, rg, _, tg = g.step(a)
+        oo, ro, _, to = o.step(a.cpu().numpy()[idx])
+        np.testing.assert_array_equal(tg.cpu().numpy()[idx], to)
+        eqs.append(np.abs(g.get_state()["qpos"].cpu().numpy()[idx] - o.get_state()["qpos"]).max(axis=1))
+        ers.append(np.abs(rg.cpu().numpy()[idx] - ro))
+        np.testing.assert_array_equal(og.cpu().numpy()[idx][:, lay["fingering"]], oo[:, lay["fingering"]])
+    eq, er = np.concatenate(eqs), np.concatenate(ers)
+    assert np.median(eq) < 1e-5 and np.percentile(eq, 99) < 1e-4, (np.median(eq), np.percentile(eq, 99), eq.max())
+    assert np.percentile(er, 99) < 1e-3, er.max()
 
 
 def test_config1_single_env_500_random_steps(dp, ref):
@@ -135,7 +141,7 @@ def test_config1_single_env_500_random_steps(dp, ref):
         errs.append(np.abs(_gs(core)["qpos"] - o.get_state()["qpos"]).max())
     assert firsts == 3
     errs, rerr = np.array(errs), np.array(rerr)
-    assert np.median(errs) < 1e-5 and np.percentile(errs, 99) < 1e-3, (np.median(errs), errs.max())
+    assert np.median(errs) < 1e-5 and np.percentile(errs, 99) < 1e-4, (np.median(errs), np.percentile(errs, 99), errs.max())
     assert np.percentile(rerr, 99) < 1e-3, rerr.max()
 
 
@@ -164,7 +170,7 @@ def test_randomize_hand_positions_parity(dp, ref):
         o.step(a)
         errs.append(np.abs(_gs(g)["qpos"] - o.get_state()["qpos"]).max(axis=1))
     e = np.concatenate(errs)
-    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-3, (np.median(e), e.max())
+    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
     # an auto-reset draws the next episode's shift
     g.set_state({"t_idx": np.full(n, st.T - 1, np.int32)})
     g.step(torch.zeros(n, 45, device="cuda:0"))
@@ -211,3 +217,74 @@ def test_non_finite_actions_do_not_stall_the_launch(dp):
         outs.append((g.get_state()["qpos"].cpu().numpy(), obs.cpu().numpy(), rew.cpu().numpy()))
     (q0, o0, r0), (q1, o1, r1) = outs
     assert np.array_equal(q0[6:], q1[6:]) and np.array_equal(o0[6:], o1[6:]) and np.array_equal(r0[6:], r1[6:])
+
+
+def _poison(s):
+    """env 0: NaN hand joint, env 1: inf key angle, env 2: |qvel| > 1e10 (mj_checkPos / checkVel)."""
+    s = {k: v.copy() for k, v in s.items()}
+    s["qpos"][0, 100] = np.nan
+    s["qpos"][1, 7] = np.inf
+    s["qvel"][2, 120] = 3e10
+    return s
+
+
+def test_diverged_envs_reset_and_flagged(dp, ref):
+    """MuJoCo resets a diverged env's data and raises a warning (mj_checkPos / mj_checkVel); the
+    kernel does the same per env and counts it (ps_warnings), like the oracle; the other envs
+    step bit-identically to an unpoisoned run, and the reset envs match the oracle's."""
+    N = 16
+    seq = song(dp, "crossing_field")
+    task = dp.TaskConfig(trim_silence=True)
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    lo, hi = dp.model.action_spec(md)
+    rng = np.random.RandomState(4)
+    acts = [rng.uniform(lo, hi, (N, 45)).astype(np.float32) for _ in range(5)]
+    o = ref.OracleEnv(md, st, tc, N)
+    o.reset()
+    for a in acts[:3]:
+        o.step(a)
+    s0 = o.get_state()
+    runs = []
+    for poison in (False, True):
+        g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", canonical_actions=False)
+        g.reset()
+        g.set_state(_poison(s0) if poison else s0)
+        for a in acts[3:]:
+            g.step(torch.from_numpy(a).cuda())
+        runs.append((_gs(g), g.warnings().cpu().numpy()))
+    (sc, wc), (sp, wp) = runs
+    assert (wc == 0).all()
+    exp = np.zeros((N, 3), np.int32)
+    exp[0, 0] = exp[1, 0] = exp[2, 1] = 1
+    np.testing.assert_array_equal(wp, exp)
+    for k in ("qpos", "qvel"):
+        assert np.isfinite(sp[k]).all()
+        np.testing.assert_array_equal(sp[k][3:], sc[k][3:])
+    o.set_state(_poison(s0))
+    for a in acts[3:]:
+        o.step(a)
+    np.testing.assert_array_equal(o.warnings(), exp)
+    e = np.abs(sp["qpos"][:3] - o.get_state()["qpos"][:3]).max()
+    assert e < 1e-4, e
+
+
+def test_environment_raises_physics_error(dp):
+    """composer.Environment.step: a physics warning raises PhysicsError by default; with
+    raise_exception_on_physics_error=False the step ends the episode (LAST, reward 0, discount
+    0) and the next step resets (FIRST)."""
+    for raise_ in (True, False):
+        env = dp.envs.Environment(song(dp, "twinkle"), dp.TaskConfig(), raise_exception_on_physics_error=raise_)
+        env.reset()
+        a = np.zeros(45, np.float32)
+        assert env.step(a).mid()
+        q = env.core.get_state()["qvel"]
+        q[0, 90] = float("nan")
+        env.core.set_state({"qvel": q})
+        if raise_:
+            with pytest.raises(dp.PhysicsError, match="BADQVEL"):
+                env.step(a)
+        else:
+            ts = env.step(a)
+            assert ts.last() and ts.reward == 0.0 and ts.discount == 0.0
+            assert env.step(a).first()
+            assert env.step(a).mid()

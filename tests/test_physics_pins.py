@@ -99,3 +99,71 @@ def test_equilibrium_formula_self_consistent(dp):
         a_s = smooth_force(p, qs, 0.0) / p["M"]
         f = max(0.0, -(a_s - aref) / (1.0 / p["M"] + R))
         assert abs(a_s + f / p["M"]) < 1e-9 * abs(a_s)
+
+
+# ------------------------------------------------------------------ joint friction loss
+FL_DOFS = (5, 21)  # FFJ3 and THJ5 of each hand: ranges contain 0, so qpos0 has no limit row
+
+
+def frictionloss_task(dp, fl_by_dof):
+    """The authored hand with frictionloss only on the given dofs (both hands), through the MJCF
+    path; one physics substep per control step."""
+    hand = dp.model.authored_hand()
+    dofs = [d._replace(frictionloss=fl_by_dof.get(j, 0.0)) if hasattr(d, "_replace") else
+            __import__("dataclasses").replace(d, frictionloss=fl_by_dof.get(j, 0.0)) for j, d in enumerate(hand.dofs)]
+    return dp.TaskConfig(hand_xml=dp.mjcf.hand_to_mjcf(hand._replace(dofs=dofs)), control_timestep=0.005)
+
+
+def frictionloss_state(n, vel):
+    """qpos0 (keys up, hands in their default pose, in the air), dof velocities `vel` {dof: v}."""
+    s = state(n, np.zeros(88))
+    for h in range(2):
+        for j, v in vel.items():
+            s["qvel"][:, 88 + 26 * h + j] = v
+    return s
+
+
+def frictionloss_cases(dp, run):
+    """Known answers of one friction-loss row (analytic.frictionloss_qacc): each dof of FL_DOFS
+    alone (one row per hand: the hands are independent) at qpos0, at rest and moving, with the
+    bound 10x above the creep force (regularised stick) and at 0.3x of it (slip at the saturated
+    force). ``run(task, state) -> qacc_ws [140]`` steps one substep on the oracle or the GPU.
+    Returns [(measured, expected, regime)]."""
+    from analytic import frictionloss_qacc
+    out = []
+    task0 = frictionloss_task(dp, {})
+    md0, _, _ = dp.compile_task(song(dp, "twinkle"), task0, canonical_actions=False)
+    for j in FL_DOFS:
+        for v in (0.0, 0.5):
+            s = frictionloss_state(1, {j: v})
+            xs = run(task0, s)
+            _, fu, _ = frictionloss_qacc(md0, xs[88 + j], md0.dof_invweight[0][j], np.inf, v)
+            for scale in (10.0, 0.3):
+                fl = float(scale * abs(fu))
+                task = frictionloss_task(dp, {j: fl})
+                md, _, _ = dp.compile_task(song(dp, "twinkle"), task, canonical_actions=False)
+                x = run(task, s)
+                for h in range(2):
+                    i = 88 + 26 * h + j
+                    e, f, regime = frictionloss_qacc(md, xs[i], md.dof_invweight[h][j], fl, v)
+                    assert regime == ("creep" if scale > 1 else "slip")
+                    out.append((x[i], e, regime))
+    return out
+
+
+def test_frictionloss_single_row_known_answers(dp, ref):
+    """a hinge with frictionloss under a constant (gravity) torque, below
+    the threshold (regularised creep: qacc = (1 - d0) qacc_smooth at rest) and above it (slip:
+    qacc = qacc_smooth - A frictionloss sign), at rest and moving (aref = -b v)."""
+    def run(task, s):
+        md, st, tc = dp.compile_task(song(dp, "twinkle"), task, canonical_actions=False)
+        env = ref.OracleEnv(md, st, tc, 1)
+        env.set_state(s)
+        assert env.contacts(0) == []
+        env.step(np.zeros((1, 45), np.float32))
+        return env.get_state()["qacc_ws"][0]
+
+    cases = frictionloss_cases(dp, run)
+    assert {r for _, _, r in cases} == {"creep", "slip"}
+    for got, exp, regime in cases:
+        assert abs(got - exp) <= 1e-9 * max(1.0, abs(exp)), (got, exp, regime)

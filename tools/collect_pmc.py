@@ -50,7 +50,9 @@ def main():
     write_kb = counter(wdir, "WRITE_SIZE")
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     from bench import lib_sha  # the profiled binary (bench.py quotes only profiles of its own build)
-    out = {"envs": envs, "song": song, "kernel": "pianosim_kernel", "lib_sha": lib_sha()}
+    import os
+    hand = "hull" if os.environ.get("PIANOSIM_HULL") else "authored"  # bench.py --hand
+    out = {"envs": envs, "song": song, "hand": hand, "kernel": "pianosim_kernel", "lib_sha": lib_sha()}
     if stats:
         s = stats[0]
         out["rocprof_avg_ns_all_launches"] = float(s.get("AverageNs", 0))
@@ -82,7 +84,8 @@ def main():
             w.writeheader()
             w.writerows(rows(tdir, "*kernel_stats.csv"))
     Path(f"profiles/{prefix}_pmc.json").write_text(json.dumps(out, indent=1))
-    Path("profiles/pmc_latest.json").write_text(json.dumps(out, indent=1))
+    if hand == "authored":  # the bench's default workload; the hull hand's summary stays under its prefix
+        Path("profiles/pmc_latest.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out))
 
 

@@ -12,7 +12,8 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 L = lib.load()
 L.ps_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
 NAME = sys.argv[2] if len(sys.argv) > 2 else "crossing_field"
-g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle"), device="cuda:0")
+g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle", **(
+    {"hand_xml": dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand())} if __import__("os").environ.get("PIANOSIM_HULL") else {})), device="cuda:0")
 g.reset()
 L.ps_debug_timing(g._h, None)
 gen = torch.Generator(device="cuda:0").manual_seed(1)

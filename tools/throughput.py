@@ -16,10 +16,11 @@ from helpers import song  # noqa: E402
 
 def throughput(name, n, steps=20):
     import os
-    solver = os.environ.get("PIANOSIM_SOLVER", "exact")  # "pgs": the round-1 solver (A/B against old builds)
-    warm = os.environ.get("PIANOSIM_WARMUP")  # warm-up PGS sweeps of the exact solve (default 8)
-    task = dp.TaskConfig(trim_silence=name != "twinkle", constraint_solver=solver,
-                         pgs_iterations=None if warm is None else int(warm))
+    its = os.environ.get("PIANOSIM_NEWTON_ITERS")  # Newton iteration cap (default: the library's)
+    task = dp.TaskConfig(trim_silence=name != "twinkle",
+                         solver_iterations=None if its is None else int(its))
+    if os.environ.get("PIANOSIM_HULL"):  # the box / hull-fingertip hand (reference default colliders)
+        task = dp.TaskConfig(trim_silence=name != "twinkle", hand_xml=dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand()))
     g = dp.BatchedPianoEnv(n, song(dp, name), task, device="cuda:0")
     g.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(12345)
@@ -37,7 +38,7 @@ def throughput(name, n, steps=20):
     r = sorted(rates)[2]
     lib = Path(dp._lib.LIB_PATH).name
     print(f"{name:15s} N={n:6d}: {r:12,.0f} env-steps/s ({n / r * 1e3:.3f} ms/step) "
-          f"[min {min(rates):,.0f} max {max(rates):,.0f}] {lib} solver={solver} warmup={task.pgs_iterations}", flush=True)
+          f"[min {min(rates):,.0f} max {max(rates):,.0f}] {lib} iters={task.solver_iterations}", flush=True)
 
 
 if __name__ == "__main__":
