@@ -1177,7 +1177,7 @@ long ref_found_hist[REF_HIST];
 long ref_cap_events[1];
 long ref_iter_total, ref_substeps_total;
 long ref_newton_hist[64];     /* Newton iterations per substep ([63]: iteration cap) */
-long ref_zone_counts[6];      /* study: rows at the solution by type (friction, limit, contact edge) x (outside, quadratic zone) */
+long ref_zone_counts[6 + 128];      /* study: rows at the solution by type (friction, limit, contact edge) x (outside, quadratic zone) */
 void ref_zone_stats(long* out) { memcpy(out, ref_zone_counts, sizeof(ref_zone_counts)); memset(ref_zone_counts, 0, sizeof(ref_zone_counts)); }
 long ref_warnings_total[PS_NWARN];
 /* Study override of the constraint solve:
@@ -1383,12 +1383,17 @@ static int newton_solve(const model* m, envdata* E, int nr, const int* dofs, int
     if (step <= 1e-15 * xmag) { ret = iter; break; }  /* at the rounding floor of x */
     (void)row_cost;
   }
-  /* study: rows in their quadratic zone at the solution, by type (ref_zone_stats) */
+  /* study: rows in their quadratic zone at the solution, by type (ref_zone_stats), and a
+   * histogram of their number per substep */
+  int nq = 0;
   for (int r = 0; r < nr; r++) {
     if (g_rows[r].closed) continue;
     double j = dotv(g_rows[r].J, x) - g_rows[r].aref;
-    __atomic_fetch_add(&ref_zone_counts[2 * g_rows[r].type + (row_quad(&g_rows[r], j) ? 1 : 0)], 1, __ATOMIC_RELAXED);
+    int q = row_quad(&g_rows[r], j) ? 1 : 0;
+    nq += q;
+    __atomic_fetch_add(&ref_zone_counts[2 * g_rows[r].type + q], 1, __ATOMIC_RELAXED);
   }
+  __atomic_fetch_add(&ref_zone_counts[6 + (nq < 127 ? nq : 127)], 1, __ATOMIC_RELAXED);
   return ret;
 }
 
