@@ -56,6 +56,7 @@ struct ps_env {
   int* episode;             // resets so far per env (the draw counter)
   int* stats;               // [N][PS_NSTATS] solver / cap counters of the last step
   int* warnings;            // [N][PS_NWARN] physics warnings since create
+  float* park;              // [N][PARK_WORDS][64] kernel scratch (lane state around the Newton solve)
   uint64_t seed;
   bool has_x;               // box / hull colliders: the pianosim_kernel<true> instantiation
   Contact* con_out;         // [N][MAXCON] contact lists of the last step (ps_record_contacts)
@@ -512,6 +513,7 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   HIPCHK(hipMalloc(&E->stats, sizeof(int) * N * PS_NSTATS));
   HIPCHK(hipMalloc(&E->warnings, sizeof(int) * N * PS_NWARN));
   HIPCHK(hipMemset(E->warnings, 0, sizeof(int) * N * PS_NWARN));
+  HIPCHK(hipMalloc(&E->park, sizeof(float) * N * PARK_WORDS * 64));
   HIPCHK(hipMemset(E->hand_dy, 0, sizeof(float) * N));
   HIPCHK(hipMemset(E->episode, 0, sizeof(int) * N));
   HIPCHK(hipMemset(E->stats, 0, sizeof(int) * N * PS_NSTATS));
@@ -546,7 +548,7 @@ void ps_destroy(ps_env* E) {
   hipFree(E->qpos); hipFree(E->qvel); hipFree(E->qws); hipFree(E->applied); hipFree(E->ctrl); hipFree(E->sustain);
   hipFree(E->terms); hipFree(E->tips); hipFree(E->t_idx); hipFree(E->ncon); hipFree(E->last);
   hipFree(E->mus_acc); hipFree(E->mus_ep); hipFree(E->mus_cnt); hipFree(E->order);
-  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats); hipFree(E->warnings);
+  hipFree(E->hand_dy); hipFree(E->episode); hipFree(E->stats); hipFree(E->warnings); hipFree(E->park);
   if (E->con_out) hipFree(E->con_out);
   delete E;
 }
@@ -598,7 +600,7 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
           (uint32_t)E->seed, (uint32_t)(E->seed >> 32), (uint32_t)E->env_offset, E->full_cpl};
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt,
-         E->hand_dy, E->episode, E->stats, E->con_out, E->warnings};
+         E->hand_dy, E->episode, E->stats, E->con_out, E->warnings, E->park};
   const int* order = nullptr;
   if (mode == 0 && E->ordered && E->n >= 2048) {  // below one wave of workgroups there is no tail to balance
     hipLaunchKernelGGL(order_kernel, dim3(1), dim3(ORDER_THREADS), 0, (hipStream_t)stream, E->stats, E->last, E->order,
