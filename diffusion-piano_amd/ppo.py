@@ -552,6 +552,7 @@ class PPOAgent:
         self._offset = 0
         self._cap = 0
         self._graph = None
+        self._chunk_graph = None
         self._graph_eager_left = 2
         self._cap_stream = torch.cuda.Stream(self.device)
         self.last_update_log = None
@@ -639,6 +640,22 @@ class PPOAgent:
                 self._clip_step()
         self._graph = (g1, g2)
 
+    # full-size minibatch steps per captured graph once the single-step graph exists (single
+    # GPU): one index upload, one replay and one log copy per CHUNK steps instead of per step
+    CHUNK = 8
+
+    def _capture_chunk(self):
+        """CHUNK consecutive minibatch steps as ONE graph: step j reads its indices from
+        ``_idx_chunk[j B:(j + 1) B]`` and logs into ``_log_chunk[j]``; the same launches in the
+        same order as CHUNK single-step replays (bitwise the same update)."""
+        B = self.batch_size
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle(), stream=self._cap_stream):
+            for j in range(self.CHUNK):
+                self._forward_backward(self._idx_chunk[j * B:(j + 1) * B], self._log_chunk[j])
+                self._clip_step()
+        self._chunk_graph = g
+
     def _replay(self):
         g1, g2 = self._graph
         g1.replay()
@@ -657,8 +674,11 @@ class PPOAgent:
         self._ADV = torch.empty(n, **f32)
         self._RET = torch.empty(n, **f32)
         self._idx = torch.zeros(self.batch_size, device=self.device, dtype=torch.int64)
+        self._idx_chunk = torch.zeros(self.CHUNK * self.batch_size, device=self.device, dtype=torch.int64)
         self._log_row = torch.zeros(len(LOG_KEYS), **f32)
+        self._log_chunk = torch.zeros(self.CHUNK, len(LOG_KEYS), **f32)
         self._graph = None  # buffers moved: re-capture
+        self._chunk_graph = None
         self._fused = None
         self._graph_eager_left = 2
 
@@ -718,10 +738,23 @@ class PPOAgent:
         nmb = (n + B - 1) // B
         log = torch.empty(self.ppo_epochs * nmb, len(LOG_KEYS), device=self.device)
         row = 0
+        nfull = n // B  # the full-size minibatches come first; only the last may be short
+        CH = self.CHUNK
         for _ in range(self.ppo_epochs):
             perm = loader_permutation(n).to(self.device, non_blocking=True)
-            for i in range(nmb):
+            i = 0
+            while i < nmb:
+                if self.graphs and not self.distributed and self._graph is not None and i + CH <= nfull:
+                    if self._chunk_graph is None:
+                        self._capture_chunk()
+                    self._idx_chunk.copy_(perm[i * B:(i + CH) * B])
+                    self._chunk_graph.replay()
+                    log[row:row + CH].copy_(self._log_chunk)
+                    i += CH
+                    row += CH
+                    continue
                 idx = perm[i * B:(i + 1) * B]
+                i += 1
                 if idx.numel() == B and self.graphs:
                     self._idx.copy_(idx)
                     if self._graph is None and self._graph_eager_left > 0:
@@ -781,6 +814,7 @@ class PPOAgent:
         if "reward_normalizer" in ck:
             self.reward_normalizer.stats.copy_(ck["reward_normalizer"])
         self._graph = None  # optimiser state tensors were replaced: re-capture
+        self._chunk_graph = None
         self._graph_eager_left = 2
 
     def save_model(self, path):

@@ -322,3 +322,31 @@ def test_rollout_trainer_masks_auto_reset_steps(ppo, tmp_path):
         tr2.iterate()
     assert calls == [True] * 4
     env.close()
+
+
+def test_chunked_graph_update_equals_eager(ppo, tmp_path):
+    """update() with graphs replays CHUNK full-size minibatch steps per graph once the
+    single-step graph exists (20 minibatches: 2 eager warm-ups, 1 single-step capture, then
+    chunks of 8, and single replays / the short tail eagerly). The same launches in the same
+    order as the eager fused step: logs and parameters bitwise equal (critic in eval mode)."""
+    rng = np.random.RandomState(11)
+    n, S, B = 20 * 16 - 5, 64, 16  # 19 full minibatches + a 11-row tail per epoch
+    s = rng.rand(n, S).astype(np.float32)
+    a = rng.uniform(-1, 1, (n, 45)).astype(np.float32)
+    lp = rng.uniform(-60, -40, n).astype(np.float32)
+    r, d = rng.rand(n), (rng.rand(n) < 0.1).astype(np.float32)
+    ns = rng.rand(n, S).astype(np.float32)
+    agents = []
+    for graphs in (True, False):
+        torch.manual_seed(0)
+        ag = ppo.PPOAgent(S, 45, batch_size=B, ppo_epochs=2, use_wandb=False, checkpoint_dir=str(tmp_path),
+                          graphs=graphs)
+        ag.critic.eval()
+        for call in range(2):
+            torch.manual_seed(100 + call)
+            ag.update(s, a, r, lp, ns, d)
+        agents.append(ag)
+    assert agents[0]._chunk_graph is not None  # the chunk path ran
+    np.testing.assert_array_equal(agents[0].last_update_log.cpu().numpy(), agents[1].last_update_log.cpu().numpy())
+    for (k, p0), (_, p1) in zip(_params(agents[0]).items(), _params(agents[1]).items()):
+        np.testing.assert_array_equal(p0.cpu().numpy(), p1.cpu().numpy(), err_msg=k)

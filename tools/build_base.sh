@@ -6,7 +6,7 @@ REV=${1:-HEAD}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
 mkdir -p "$T/pkg/csrc" "$T/include"
-for f in pianosim.hip kernel_v2.inc devmodel.h prims.h collide_x.h; do
+for f in pianosim.hip kernel_v2.inc newton.inc devmodel.h prims.h collide_x.h; do
   git -C "$ROOT" show "$REV:diffusion-piano_amd/csrc/$f" > "$T/pkg/csrc/$f"
 done
 git -C "$ROOT" show "$REV:include/pianosim.h" > "$T/include/pianosim.h"

@@ -22,10 +22,10 @@ gen = torch.Generator(device="cuda:0").manual_seed(1)
 for _ in range(3):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
 L.ps_debug_timing(g._h, None)
-names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest", 11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs",
-         3: "factor", 4: "solve_smooth", 12: "cons:limits", 13: "cons:contact J", 14: "cons:contact L^-T",
-         15: "cons:finish", 16: "pgs:build A", 17: "pgs:sweeps", 18: "ex:rest", 19: "ex:start set",
-         23: "ex:tableau", 20: "ex:factor+solve", 21: "ex:w+check", 8: "pgs:J^T f", 6: "integrate", 5: "final+task"}
+names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest",
+         11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs", 18: "newton:prep", 3: "factor", 4: "solve_smooth",
+         12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
+         8: "nt:J'f", 6: "integrate", 5: "final+task"}  # the slots of phase_timing.py (Newton solve)
 idx = list(names)
 out = np.zeros((N, 28), np.uint64)
 means, maxes, worst_rows, mean_rows, ms, piv = [], [], [], [], [], []
@@ -53,7 +53,7 @@ print(f"# tools/tail_timing.py {N} {NAME}: {STEPS} steps, per-step mean env vs s
 print(f"launch ms (timing build) mean {np.mean(ms):.3f}; mean env {mt.mean():.0f}, slowest env {xt.mean():.0f} "
       f"(ratio {xt.mean() / mt.mean():.2f}, per step min {np.min(xt / mt):.2f} max {np.max(xt / mt):.2f}); "
       f"rows/substep mean env {np.mean(mean_rows):.1f}, slowest env {np.mean(worst_rows):.1f}")
-print(f"principal pivots per env-step: mean env {np.mean([a for a, b in piv]):.1f}, slowest env {np.mean([b for a, b in piv]):.1f}")
+print(f"(slot 22, unused since the Newton solve) mean env {np.mean([a for a, b in piv]):.1f}, slowest env {np.mean([b for a, b in piv]):.1f}")
 print(f"{'phase':18s} {'mean env':>10s} {'slowest':>10s} {'excess':>10s}")
 for j, i in enumerate(idx):
     print(f"{names[i]:18s} {means[:, j].mean():10.0f} {maxes[:, j].mean():10.0f} {maxes[:, j].mean() - means[:, j].mean():10.0f}")
