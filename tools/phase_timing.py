@@ -37,6 +37,12 @@ solves = st[..., 0] / 10.0
 print(f"Newton: iterations per substep mean {solves.mean():.3f}, max over env-steps {st[..., 0].max()} per step; "
       f"contact-cap substeps {int(st[..., 1].sum())}, iteration-cap substeps {int(st[..., 2].sum())}, "
       f"max contact rows {int(st[..., 3].max())}, coupled substeps {st[..., 4].sum() / (10 * st[..., 4].size):.3f}")
+# iterations by substep (timing-build counters 19-23): the first substep starts cold, the later
+# ones from the previous substep's zones (one iteration when that piece holds)
+c = out[:, 19:24].astype(np.float64).sum(axis=0)
+if c[1] > 0 and c[4] > 0:
+    print(f"Newton by substep: first {c[0] / c[1]:.2f} iterations, later {c[2] / c[4]:.2f} "
+          f"(guessed piece held in {100 * c[3] / c[4]:.1f}% of the later substeps)")
 # the per-env spread sets the tail of a launch (4096 envs = 2 rounds of 2048 slots)
 per = tot / 10
 q = np.percentile(per, [50, 90, 99, 100])
