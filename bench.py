@@ -114,6 +114,24 @@ def cpu_baseline(dp, seq, task, n_envs, steps):
     return out
 
 
+def oracle_sha() -> str:
+    """sha256 (16 hex) of the physics a CPU-side profile was measured on: the checker's source
+    text and the compiled default model (ps_model_desc bytes); tools/chaos_floor.py records the
+    same. Reads the checker's file text only."""
+    import ctypes
+    import hashlib
+
+    sys.path.insert(0, str(ROOT))
+    model = importlib.import_module("diffusion-piano_amd.model")
+    h = hashlib.sha256()
+    try:
+        h.update((ROOT / "oracle" / "pianosim_ref.c").read_bytes())
+    except OSError:
+        return "missing"
+    h.update(ctypes.string_at(ctypes.addressof(md := model.build_model()), ctypes.sizeof(md)))
+    return h.hexdigest()[:16]
+
+
 def lib_sha(path=None) -> str:
     """sha256 (16 hex) of the step kernel's library: profiles record it, and the bench only
     quotes a profile measured on the very binary it runs."""
@@ -187,6 +205,8 @@ def drift_summary(sha):
     out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"), "song": d.get("song"),
            "source": "profiles/drift_latest.json (tests/test_gpu_drift.py, same library build)"}
     chaos = _profile("chaos_floor.json") or {}
+    if chaos.get("oracle_sha") != oracle_sha():  # measured on other physics: not this floor
+        chaos = {}
     for k in ("zero_action", "trace_actions", "random_actions"):
         if k in d:
             out[k] = {"teacher_forced_p99": d[k]["teacher_forced_qpos_linf"]["p99"],
@@ -329,7 +349,8 @@ def main():
                                             "newton_cap_substeps": int(stats[:, 2].sum()),
                                             "max_contact_rows": int(stats[:, 3].max()),
                                             "coupled_substep_frac": float(stats[:, 4].sum() / (10.0 * stats.shape[0])),
-                                            "bad_pivot_substeps": int(stats[:, 5].sum())}},
+                                            "bad_pivot_substeps": int(stats[:, 5].sum()),
+                                            "max_coupled_dofs": int(stats[:, 6].max())}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,

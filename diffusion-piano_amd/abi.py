@@ -22,9 +22,10 @@ GEOM_NONE, GEOM_BOX, GEOM_HULL = 0, 1, 2
 MAX_NOTES = 16
 MAX_CONTACTS_LIMIT = 24
 NTERMS = 5
-NSTATS = 6  # ps_solver_stats slots (PS_STAT_*): Newton iterations, contact-cap substeps, iteration-cap
-            # substeps, most rows in a substep, hand-coupled substeps, non-positive pivots
-STAT_SOLVES, STAT_CONTACT_CAP, STAT_ITER_CAP, STAT_MAX_ROWS, STAT_COUPLED, STAT_BAD_PIVOT = range(6)
+NSTATS = 7  # ps_solver_stats slots (PS_STAT_*): Newton iterations, contact-cap substeps, iteration-cap
+            # substeps, most contact rows in a substep, hand-coupled substeps, non-positive pivots,
+            # most coupled dofs in a substep
+STAT_SOLVES, STAT_CONTACT_CAP, STAT_ITER_CAP, STAT_MAX_ROWS, STAT_COUPLED, STAT_BAD_PIVOT, STAT_MAX_CDOFS = range(7)
 NWARN = 3  # ps_warnings slots: mj_checkPos / mj_checkVel / mj_checkAcc resets
 WARN_BADQPOS, WARN_BADQVEL, WARN_BADQACC = range(3)
 NMUSIC = 6  # ps_musical_metrics slots: precision, recall, f1, sustain_precision, sustain_recall, sustain_f1
@@ -83,7 +84,7 @@ class ModelDesc(C.Structure):
         ("xgeom_vert", _arr(i32, NHAND, HAND_NXGEOM, 2)), ("hull_vert", _arr(d, NHAND, HAND_HULLVERT, 3)),
         ("n_xpairs", i32), ("xpair", _arr(i32, MAX_XPAIRS, 2)),
         ("dof_frictionloss", _arr(d, NHAND, HAND_NDOF)), ("friction_solref", _arr(d, 2)),
-        ("friction_solimp", _arr(d, 5)),
+        ("friction_solimp", _arr(d, 5)), ("hand_gravcomp", d),
     ]
 
 

@@ -41,6 +41,7 @@ struct DevModel {
   float timestep;
   int nsub;
   float grav[3];
+  float hgrav[3];  // gravity the hand bodies feel: grav (1 - hand_gravcomp)
   // keys
   float key_pos[NK][3], key_half[NK][3], key_anchor[NK][3];
   float key_mass[NK], key_Minv[NK], key_Mhinv[NK], key_damp[NK], key_stiff[NK], key_sref[NK];

@@ -97,6 +97,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
   m->nsub = d->n_substeps;
   if (m->nsub < 1) return fail("n_substeps must be >= 1");
   for (int i = 0; i < 3; i++) m->grav[i] = (float)d->gravity[i];
+  for (int i = 0; i < 3; i++) m->hgrav[i] = (float)(d->gravity[i] * (1.0 - d->hand_gravcomp));
   for (int k = 0; k < NK; k++) {
     for (int i = 0; i < 3; i++) {
       m->key_pos[k][i] = (float)d->key_pos[k][i];

@@ -99,11 +99,20 @@ class TaskConfig:
     # Constraint solve: "newton" (alias "exact") = MuJoCo's primal problem minimised by Newton
     # iterations with exact line search (mj_solNewton), to convergence - the unique solution
     # every MuJoCo solver converges to. `solver_iterations` caps the Newton iterations per
-    # substep (None: the library default, 16). The round-1 truncated "pgs" is retired.
+    # substep (None: the library default, 24). The round-1 truncated "pgs" is retired.
     constraint_solver: str = "newton"
     solver_iterations: Optional[int] = None
     max_contacts: int = 20
     hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
+    # PianoTask keyword arguments (tasks/base.py:96-107, forwarded by PianoWithShadowHands'
+    # **kwargs, piano_with_shadow_hands.py:65):
+    gravity_compensation: bool = False  # gravcomp 1 on every hand body (tasks/base.py:185-186)
+    attachment_yaw: float = model_lib.ATTACHMENT_YAW  # degrees, hand roots about z (tasks/base.py:174-181)
+    # Fingertip colliders (shadow_hand.py:95,144-152). None: the authored hand (capsules
+    # everywhere, this implementation's default); True: Menagerie-style palm boxes with capsule
+    # distal colliders; False (the reference's default): palm boxes with convex-hull (mesh)
+    # distal colliders, the step kernel's hull instantiation. Exclusive with hand_xml.
+    primitive_fingertip_collisions: Optional[bool] = None
 
     def lookahead(self) -> int:
         if self.n_seconds_lookahead is not None:
@@ -129,12 +138,19 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
             seq = music.trim_silence(seq)
         song = music.song_tables(seq, cfg.control_timestep, cfg.initial_buffer_time)
     hand = None
+    if cfg.hand_xml is not None and cfg.primitive_fingertip_collisions is not None:
+        raise ValueError("hand_xml and primitive_fingertip_collisions are exclusive: the MJCF names its colliders")
     if cfg.hand_xml is not None:
         from . import mjcf
         hand = mjcf.load_hand(cfg.hand_xml)
+    elif cfg.primitive_fingertip_collisions is not None:
+        from . import mjcf
+        hand = mjcf.box_hull_hand(hull_fingertips=not cfg.primitive_fingertip_collisions)
     md = model_lib.build_model(control_timestep=cfg.control_timestep,
                                physics_timestep=cfg.physics_timestep,
-                               hand_collisions=not cfg.disable_hand_collisions, hand=hand)
+                               hand_collisions=not cfg.disable_hand_collisions, hand=hand,
+                               gravity_compensation=cfg.gravity_compensation,
+                               attachment_yaw=cfg.attachment_yaw)
     tc = abi.TaskCfg()
     tc.n_steps_lookahead = cfg.lookahead()
     tc.fingering_reward = int(not cfg.disable_fingering_reward and song.has_fingering)
@@ -333,9 +349,10 @@ class BatchedPianoEnv:
         return t
 
     def solver_stats(self):
-        """[N, 6] int32 counters of each env's last step (PS_STAT_*): Newton iterations, substeps
+        """[N, 7] int32 counters of each env's last step (PS_STAT_*): Newton iterations, substeps
         at the contact cap, substeps at the Newton iteration cap, most contact rows, substeps with
-        the hands coupled, substeps with a non-positive Hessian pivot."""
+        the hands coupled, substeps with a non-positive Hessian pivot, most coupled dofs of both
+        hands in a substep."""
         t = self._torch.empty(self.num_envs, abi.NSTATS, device=self.device, dtype=self._torch.int32)
         _lib.check(_lib.load().ps_solver_stats(self._h, t.data_ptr(), self.stream))
         return t

@@ -683,13 +683,16 @@ def capsule_points(radius, halflen, n_ring=8, n_lat=2) -> np.ndarray:
     return np.asarray(pts)
 
 
-def box_hull_hand() -> M.HandSpec:
-    """The authored right hand with the reference's default collider kinds
-    (``primitive_fingertip_collisions=False``, shadow_hand.py:95,144-152: Menagerie palm boxes
-    and distal meshes): the two palm capsules and the little-finger metacarpal capsule become
-    boxes, every distal capsule a 58-point capsule-shaped convex hull (MuJoCo collides a mesh as
-    its hull). ``TaskConfig(hand_xml=hand_to_mjcf(box_hull_hand()))`` runs it through the MJCF
-    path; the step kernel's hull instantiation (pianosim_kernel<true>) then runs."""
+def box_hull_hand(hull_fingertips: bool = True) -> M.HandSpec:
+    """The authored right hand with the reference's collider kinds (shadow_hand.py:95,144-152:
+    Menagerie palm boxes and distal meshes): the two palm capsules and the little-finger
+    metacarpal capsule become boxes, and with ``hull_fingertips`` (the reference's default
+    ``primitive_fingertip_collisions=False``) every distal capsule a 58-point capsule-shaped convex
+    hull (MuJoCo collides a mesh as its hull); without, the distal colliders stay capsules (the
+    reference's ``primitive_fingertip_collisions=True`` turns its distal meshes into capsules).
+    ``TaskConfig(primitive_fingertip_collisions=...)`` selects it, as does
+    ``TaskConfig(hand_xml=hand_to_mjcf(box_hull_hand()))`` through the MJCF path; the step kernel's
+    box / hull instantiation (pianosim_kernel<true>) then runs."""
     hand = M.authored_hand()
     geoms, xgeoms = [], []
     names = [b.name for b in hand.bodies]
@@ -698,7 +701,7 @@ def box_hull_hand() -> M.HandSpec:
         if bname == "palm" or bname == "lfmetacarpal":
             q = _quat_from_z(g.axis)
             xgeoms.append(M.XGeom(g.body, "box", tuple(g.pos), tuple(q), (g.radius, g.radius * 0.8, g.halflen + g.radius)))
-        elif bname.endswith("distal"):
+        elif bname.endswith("distal") and hull_fingertips:
             c, v = convex_hull_collider(capsule_points(g.radius, g.halflen))
             R = M.quat_to_mat(_quat_from_z(g.axis))
             pos = np.asarray(g.pos) + R @ c

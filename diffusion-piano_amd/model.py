@@ -67,6 +67,7 @@ PHYSICS_TIMESTEP = 0.005  # tasks/base.py:28
 CONTROL_TIMESTEP = 0.05   # tasks/base.py:31
 HAND_POSITIONS = [(0.4, 0.15, 0.13), (0.4, -0.15, 0.13)]  # right, left (tasks/base.py:34-37)
 HAND_QUAT = (-1.0, -1.0, 1.0, 1.0)
+ATTACHMENT_YAW = 0.0  # degrees (tasks/base.py:39 _ATTACHMENT_YAW)
 FINGERTIP_OFFSET = 0.026  # shadow_hand.py:81-82
 THUMBTIP_OFFSET = 0.0275
 FOREARM_KP = 300.0  # shadow_hand.py:41-52
@@ -110,6 +111,20 @@ def piano_keys():
 def quat_normalize(q):
     q = np.asarray(q, dtype=np.float64)
     return q / np.linalg.norm(q)
+
+
+def quat_mul(a, b):
+    """Hamilton product a * b (w x y z), as mju_mulQuat."""
+    aw, ax, ay, az = a
+    bw, bx, by, bz = b
+    return (aw * bw - ax * bx - ay * by - az * bz, aw * bx + ax * bw + ay * bz - az * by,
+            aw * by - ax * bz + ay * bw + az * bx, aw * bz + ax * by - ay * bx + az * bw)
+
+
+def _quat_axisangle(axis, angle):
+    """Unit quaternion of a rotation by ``angle`` about the unit ``axis`` (mju_axisAngle2Quat)."""
+    s = math.sin(0.5 * angle)
+    return (math.cos(0.5 * angle), axis[0] * s, axis[1] * s, axis[2] * s)
 
 
 def quat_to_mat(q):
@@ -370,7 +385,8 @@ def _subtree_mass(bodies, root):
 
 
 def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: float = PHYSICS_TIMESTEP,
-                hand_collisions: bool = True, hand: Optional[HandSpec] = None) -> abi.ModelDesc:
+                hand_collisions: bool = True, hand: Optional[HandSpec] = None,
+                gravity_compensation: bool = False, attachment_yaw: float = ATTACHMENT_YAW) -> abi.ModelDesc:
     """Compile the scene into a ``ps_model_desc``.
 
     ``hand``: the right hand to use (``mjcf.load_hand`` of a user MJCF); default the authored
@@ -379,11 +395,16 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
     ``hand_collisions=False`` is ``disable_hand_collisions`` (piano_with_shadow_hands.py:476-489):
     every hand collider gets contype=1, conaffinity=0, so no hand geom pair collides
     (hands still collide with the piano, whose conaffinity is 1).
+
+    ``gravity_compensation`` (tasks/base.py:185-186): gravcomp = 1 on every hand body, a passive
+    force cancelling the hands' gravity. ``attachment_yaw`` (degrees, tasks/base.py:174-181): the
+    hand roots turned about world z by +yaw (right) / -yaw (left) before their quaternion.
     """
     m = abi.ModelDesc()
     m.timestep = physics_timestep
     m.n_substeps = int(round(control_timestep / physics_timestep))
     m.gravity[:] = (0.0, 0.0, -9.81)
+    m.hand_gravcomp = 1.0 if gravity_compensation else 0.0
     for k, (pos, half, black) in enumerate(piano_keys()):
         m.key_pos[k][:] = pos
         m.key_half[k][:] = half
@@ -416,7 +437,8 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
     bodies, dofs, geoms, excludes, sites, tendons, acts, obs_order = spec[:8]
     tcoef = spec.tendon_coef or [(1.0, 1.0)] * len(tendons)
     forearm_mass = _subtree_mass(bodies, 0)
-    root_quat = tuple(quat_normalize(HAND_QUAT))
+    root_quats = [tuple(quat_normalize(quat_mul(_quat_axisangle((0.0, 0.0, 1.0), math.radians(sg * attachment_yaw)),
+                                                 HAND_QUAT))) for sg in (1.0, -1.0)]  # right, left
     m.root_geom_count = sum(1 for g in geoms if g.body == 0)
     for h in range(abi.NHAND):
         mir = h == 1
@@ -424,7 +446,7 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
             m.body_parent[h][i] = b.parent
             if i == 0:
                 m.body_pos[h][i][:] = HAND_POSITIONS[h]
-                m.body_quat[h][i][:] = root_quat
+                m.body_quat[h][i][:] = root_quats[h]
             else:
                 m.body_pos[h][i][:] = _mirror_vec(b.pos) if mir else b.pos
                 q = quat_normalize(b.quat)

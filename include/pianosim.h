@@ -167,6 +167,10 @@ typedef struct {
    * defaults (0.02, 1) and (0.9, 0.95, 0.001, 0.5, 2) unless the XML sets them). */
   double dof_frictionloss[PS_NHAND][PS_HAND_NDOF];
   double friction_solref[2], friction_solimp[5];
+  /* MuJoCo body gravcomp of every hand body (PianoTask(gravity_compensation=True),
+   * tasks/base.py:185-186: mujoco_utils.physics_utils.compensate_gravity sets 1): a passive force
+   * -gravcomp m g at each hand body's COM, i.e. the hands feel (1 - gravcomp) of the gravity */
+  double hand_gravcomp;
 } ps_model_desc;
 
 /* Song tables: NoteTrajectory in dense form (music.py:SongTables). */
@@ -185,7 +189,7 @@ typedef struct {
   int32_t forearm_reward;           /* 1: add forearm reward term */
   int32_t wrong_press_termination;
   double energy_penalty_coef;       /* 5e-3 */
-  int32_t solver_iterations;        /* Newton iterations per substep at most (0: the default cap, 16);
+  int32_t solver_iterations;        /* Newton iterations per substep at most (0: the default cap, 24);
                                        reaching it is counted (PS_STAT_ITER_CAP) */
   int32_t max_contacts;             /* per env, <= PS_MAX_CONTACTS_LIMIT */
   int32_t canonical_actions;        /* 1: ps_step actions are in [-1,1] and are rescaled to the
@@ -244,11 +248,17 @@ typedef struct {
 #define PS_STAT_SOLVES 0        /* Newton iterations (Hessian factorizations), summed */
 #define PS_STAT_CONTACT_CAP 1   /* substeps whose narrow phase found >= max_contacts contacts */
 #define PS_STAT_ITER_CAP 2      /* substeps whose Newton solve stopped at its iteration cap */
-#define PS_STAT_MAX_ROWS 3      /* most constraint rows in one substep */
+#define PS_STAT_MAX_ROWS 3      /* most contact rows (4 pyramid edges per contact) of one
+                                   substep; the solve's other rows - one friction-loss row per hand
+                                   dof with frictionloss and the violated hand / key limits - are
+                                   not counted here */
 #define PS_STAT_COUPLED 4       /* substeps whose hands were coupled (hand-hand contact or a key
-                                   touched by both hands): the Woodbury-coupled solve */
+                                   touched by both hands): the C-block elimination after both
+                                   hands' independent pivots */
 #define PS_STAT_BAD_PIVOT 5     /* substeps with a non-positive Cholesky pivot (clamped) */
-#define PS_NSTATS 6
+#define PS_STAT_MAX_CDOFS 6     /* most coupled ("C") dofs of both hands in one substep (the dofs
+                                   the hand-hand rows act on; > 28 takes the whole-block solve) */
+#define PS_NSTATS 7
 
 typedef struct ps_env ps_env;
 

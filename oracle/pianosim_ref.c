@@ -360,7 +360,7 @@ static void dynamics(const model* m, const ps_task_cfg* cfg, envdata* E) {
         vo[b] = mk(0, 0, 0);
         for (int j = m->body_dofadr[h][b]; j >= 0 && j < m->body_dofadr[h][b] + m->body_dofnum[h][b]; j++)
           vo[b] = add(vo[b], scl(E->axis[h][j], vh[j]));
-        ac[b] = scl(g, -1.0);
+        ac[b] = scl(g, -(1.0 - d->hand_gravcomp));  /* body gravcomp cancels that share (tasks/base.py:185-186) */
       } else {
         v3 r = sub(E->o[h][b], E->o[h][p]);
         w[b] = w[p];

@@ -22,8 +22,12 @@ def _gs(g):
     return {k: v.cpu().numpy() for k, v in g.get_state().items()}
 
 
-@pytest.fixture(scope="module")
-def task(dp):
+@pytest.fixture(scope="module", params=["mjcf", "flag"])
+def task(dp, request):
+    """The box / hull hand through the MJCF path, and as TaskConfig(primitive_fingertip_collisions=
+    False) (the reference's default colliders, shadow_hand.py:95,144-152)."""
+    if request.param == "flag":
+        return dp.TaskConfig(primitive_fingertip_collisions=False)
     return dp.TaskConfig(hand_xml=dp.mjcf.hand_to_mjcf(box_hull_hand(dp)))
 
 

@@ -3,9 +3,8 @@ rows, hands coupled through hand-hand contacts), the solver counters, and bitwis
 of contacts sharing a key.
 
 Tolerances (fp32 kernel vs fp64 oracle, same state and action, one control step): qpos
-median < 1e-5, p99 < 1e-4 on the bench song; the replays of coupled-hand and heavy-contact
-env-steps (the stiffest Hessians, fp32 LDL'): median < 1e-5, p99 < 2e-4 (coupled; measured
-1.6e-4) / p90 < 1e-4 (heavy)."""
+median < 1e-5, p99 < 1e-4 on the bench song, on the replays of coupled-hand and heavy-contact
+env-steps (the stiffest Hessians, fp32 LDL') and on the whole-C-block states."""
 import numpy as np
 import pytest
 
@@ -113,8 +112,8 @@ def test_newton_heavy_states(dp, ref):
     round 2 dropped rows past 64) replayed on the oracle."""
     n, e = _replay(dp, ref, lambda st: st[:, 3] > 40)
     assert n >= 4, f"only {n} heavy env-steps"
-    print(f"{n} heavy env-steps: qpos err median {np.median(e):.2e} p90 {np.percentile(e, 90):.2e} max {e.max():.2e}")
-    assert np.median(e) < 1e-5 and np.percentile(e, 90) < 1e-4, (np.median(e), np.percentile(e, 90), e.max())
+    print(f"{n} heavy env-steps: qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}")
+    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
 
 
 def test_newton_coupled_hands(dp, ref):
@@ -123,7 +122,7 @@ def test_newton_coupled_hands(dp, ref):
     n, e = _replay(dp, ref, lambda st: st[:, 4] >= 10)
     assert n >= 16, f"only {n} coupled env-steps"
     print(f"{n} coupled env-steps: qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}")
-    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 2e-4, (np.median(e), np.percentile(e, 99), e.max())
+    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
 
 
 def test_newton_coupled_hands_full_block(dp, ref, monkeypatch):
@@ -132,7 +131,46 @@ def test_newton_coupled_hands_full_block(dp, ref, monkeypatch):
     monkeypatch.setenv("PIANOSIM_DEBUG_FULL_COUPLED", "1")
     n, e = _replay(dp, ref, lambda st: st[:, 4] >= 10, steps=8)
     assert n >= 8, f"only {n} coupled env-steps"
-    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 2e-4, (np.median(e), np.percentile(e, 99), e.max())
+    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
+
+
+def test_newton_whole_c_block_overlapping_hands(dp, ref):
+    """The right hand slid along the keyboard (forearm_tx) onto the left one: hand-hand contacts
+    across many fingers couple more than 28 dofs of both hands (PS_STAT_MAX_CDOFS), which the
+    16-column C block cannot hold, so the whole-block solve (both hands' C blocks in slot
+    layout) runs; one control step from the same state against the oracle."""
+    from helpers import random_states
+    seq = song(dp, "crossing_field")
+    task = dp.TaskConfig(trim_silence=True)
+    md, sttab, tc = dp.compile_task(seq, task, canonical_actions=False)
+    lo, hi = dp_action_spec(md)
+    rng = np.random.RandomState(11)
+    txs = np.linspace(-0.36, 0.36, 25)
+    per = 32
+    N = per * len(txs)
+    q, v = random_states(md, N, rng, vscale=0.1)
+    q[:, 88] = np.repeat(txs, per)          # right hand forearm_tx (qpos: 88 keys, rh 26, lh 26)
+    q[:, 88 + 26] = 0.0                     # left hand forearm_tx at its rest position
+    a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
+    a[:, 20] = np.clip(q[:, 88], lo[20], hi[20])  # rh forearm_tx actuator holds the slide
+    a[:, 42] = 0.0
+    st = {"qpos": q.astype(np.float32), "qvel": v.astype(np.float32), "qacc_ws": np.zeros((N, 140), np.float32),
+          "ctrl": np.zeros((N, 44), np.float32), "sustain": np.zeros(N, np.float32),
+          "t_idx": np.full(N, 5, np.int32), "last": np.zeros(N, np.uint8)}
+    g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", canonical_actions=False)
+    g.set_state(st)
+    g.step(torch.from_numpy(a).cuda())
+    stats = g.solver_stats().cpu().numpy()
+    warn = g.warnings().cpu().numpy()
+    pick = np.nonzero((stats[:, 6] > 28) & (warn.sum(1) == 0))[0][:64]
+    print(f"max coupled dofs {stats[:, 6].max()}, envs above 28: {(stats[:, 6] > 28).sum()} of {N}")
+    assert len(pick) >= 4, f"only {len(pick)} env-steps with more than 28 coupled dofs"
+    o = ref.OracleEnv(md, sttab, tc, len(pick))
+    o.set_state({k: x[pick] for k, x in st.items()})
+    o.step(a[pick])
+    e = np.abs(g.get_state()["qpos"].cpu().numpy()[pick] - o.get_state()["qpos"]).max(axis=1)
+    print(f"{len(pick)} env-steps: qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}")
+    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
 
 
 def test_same_key_contacts_bitwise_repeatable(dp, ref):

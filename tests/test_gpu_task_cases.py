@@ -107,8 +107,7 @@ def test_guren_at_4096_envs(dp, ref):
         ers.append(np.abs(rg.cpu().numpy()[idx] - ro))
         np.testing.assert_array_equal(og.cpu().numpy()[idx][:, lay["fingering"]], oo[:, lay["fingering"]])
     eq, er = np.concatenate(eqs), np.concatenate(ers)
-    # p99 < 2e-4: Guren's fingering workload at 4096 envs measured 1.4e-4 (fp32 Newton)
-    assert np.median(eq) < 1e-5 and np.percentile(eq, 99) < 2e-4, (np.median(eq), np.percentile(eq, 99), eq.max())
+    assert np.median(eq) < 1e-5 and np.percentile(eq, 99) < 1e-4, (np.median(eq), np.percentile(eq, 99), eq.max())
     assert np.percentile(er, 99) < 1e-3, er.max()
 
 
@@ -181,6 +180,42 @@ def test_randomize_hand_positions_parity(dp, ref):
     assert (e2 == 2).all()
     exp = np.array([ref.hand_offset_draw(99, i, 1) for i in range(n)], np.float32)
     np.testing.assert_array_equal(d2, exp)
+
+
+def test_sharded_handles_equal_one_handle_bitwise(dp):
+    """SURVEY 8(e) on the kernel: a job of N envs on one handle equals the same job sharded over
+    two handles (env_offset = 0 and N/2, as bench.py's ranks create them) bit for bit under
+    randomize_hand_positions - the Philox draws are keyed by the global env id, and an env's
+    step depends on nothing but its own row."""
+    n = 64
+    seq = song(dp, "twinkle")
+    task = dp.TaskConfig(randomize_hand_positions=True)
+    whole = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", seed=21)
+    halves = [dp.BatchedPianoEnv(n // 2, seq, task, device="cuda:0", seed=21, env_offset=off) for off in (0, n // 2)]
+    gen = torch.Generator(device="cuda:0").manual_seed(3)
+    outs = [whole.reset()] + [h.reset() for h in halves]
+    np.testing.assert_array_equal(outs[0].cpu().numpy(), torch.cat(outs[1:]).cpu().numpy())
+    for t in range(40):
+        a = torch.rand(n, 45, device="cuda:0", generator=gen) * 2 - 1
+        if t == 20:  # episodes end at different steps: every env auto-resets into a new draw
+            tt = (np.arange(n) % 7 + dp.compile_task(seq, task)[1].T - 7).astype(np.int32)
+            whole.set_state({"t_idx": tt})
+            for i, h in enumerate(halves):
+                h.set_state({"t_idx": tt[i * n // 2:(i + 1) * n // 2]})
+        rw = whole.step(a)
+        rh = [h.step(a[i * n // 2:(i + 1) * n // 2]) for i, h in enumerate(halves)]
+        for j in range(4):
+            np.testing.assert_array_equal(rw[j].cpu().numpy(), torch.cat([r[j] for r in rh]).cpu().numpy())
+    dw, ew = (x.cpu().numpy() for x in whole.hand_offset())
+    dh = np.concatenate([x.hand_offset()[0].cpu().numpy() for x in halves])
+    eh = np.concatenate([x.hand_offset()[1].cpu().numpy() for x in halves])
+    np.testing.assert_array_equal(dw, dh)
+    np.testing.assert_array_equal(ew, eh)
+    assert (ew >= 2).any() and np.abs(dw).max() > 0.01
+    sw = whole.get_state()
+    sh = [h.get_state() for h in halves]
+    for k in ("qpos", "qvel", "qacc_ws", "ctrl"):
+        np.testing.assert_array_equal(sw[k].cpu().numpy(), torch.cat([x[k] for x in sh]).cpu().numpy())
 
 
 def test_vectorized_env_outputs_survive_the_next_step(dp):

@@ -1,0 +1,43 @@
+"""PianoTask keyword arguments on the GPU (tests/test_task_kwargs.py pins them on the checker):
+gravity_compensation, attachment_yaw and primitive_fingertip_collisions=True (palm boxes,
+capsule fingertips: the box / hull kernel instantiation), each teacher-forced against the
+checker for one control step at a time: qpos median < 1e-5, p99 < 1e-4; rewards p99 < 1e-3.
+(primitive_fingertip_collisions=False, the hull fingertips: tests/test_gpu_colliders.py.)"""
+import numpy as np
+import pytest
+
+from helpers import song
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+KEYS = ("qpos", "qvel", "qacc_ws", "ctrl", "sustain", "t_idx", "last")
+
+
+@pytest.mark.parametrize("kw", [dict(gravity_compensation=True), dict(attachment_yaw=15.0),
+                                dict(primitive_fingertip_collisions=True)], ids=["gravcomp", "yaw", "primitive"])
+def test_task_kwargs_teacher_forced(dp, ref, kw):
+    n = 32
+    seq = song(dp, "twinkle")
+    task = dp.TaskConfig(**kw)
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
+    o = ref.OracleEnv(md, st, tc, n)
+    lo, hi = dp.model.action_spec(md)
+    rng = np.random.RandomState(17)
+    g.reset()
+    o.reset()
+    np.testing.assert_allclose(g.fingertips().cpu().numpy(), o.fingertips(), atol=2e-6)
+    errs, rerr, ncon = [], [], 0
+    for _ in range(12):
+        a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
+        o.set_state({k: v.cpu().numpy() for k, v in g.get_state().items() if k in KEYS})
+        _, rg, _, _ = g.step(torch.from_numpy(a).cuda())
+        _, ro, _, _ = o.step(a)
+        errs.append(np.abs(g.get_state()["qpos"].cpu().numpy() - o.get_state()["qpos"]).max(axis=1))
+        rerr.append(np.abs(rg.cpu().numpy() - ro))
+        ncon += int(o.contact_count().sum())
+    e, r = np.concatenate(errs), np.concatenate(rerr)
+    assert ncon > 0
+    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
+    assert np.percentile(r, 99) < 1e-3, r.max()

@@ -58,10 +58,17 @@ def run(dp, kind, delta):
     return {"qpos_linf_at_step": out, "max_over_1000": worst}
 
 
+def oracle_sha():
+    """The physics the floor is measured on (bench.py's oracle_sha: the checker's source and the
+    compiled default model); bench.py drops a floor whose hash differs."""
+    from bench import oracle_sha as sha
+    return sha()
+
+
 def main():
     dp = importlib.import_module("diffusion-piano_amd")
     rep = {"checker": "fp64 C restatement vs itself, hand qpos perturbed by +-delta at each episode start",
-           "envs": N, "steps": STEPS, "song": "twinkle"}
+           "envs": N, "steps": STEPS, "song": "twinkle", "oracle_sha": oracle_sha()}
     for kind in ("zero", "trace", "random"):
         for delta in (1e-12, 1e-7):
             rep[f"{kind}/delta={delta:g}"] = run(dp, kind, delta)

@@ -1,0 +1,121 @@
+"""Teacher-forced qpos error of the GPU step against the fp64 oracle on the workloads the GPU
+parity gates hold (development aid; the gates themselves are the tests):
+
+  bench    tests/test_gpu_solver.py::test_exact_solver_teacher_forced_bench_song (64 CF envs, 8 steps)
+  coupled  test_newton_coupled_hands (replays of env-steps whose every substep coupled the hands)
+  heavy    test_newton_heavy_states (replays of env-steps with > 40 contact rows)
+  trace    test_gpu_drift.py teacher-forced part, the reference's Twinkle action trace (8 envs, 200 steps)
+  random   the same with uniform random actions
+  guren    test_gpu_task_cases.py::test_guren_at_4096_envs (64 sampled of 4096 envs, 4 steps)
+
+usage: PIANOSIM_LIB=diffusion-piano_amd/<lib>.so python tools/parity_probe.py [case ...]
+Prints one JSON line per case (median / p99 / max of the per-env-step qpos L-inf error)."""
+import importlib
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+sys.path.insert(0, str(ROOT / "oracle"))
+dp = importlib.import_module("diffusion-piano_amd")
+import ref  # noqa: E402  (oracle/ref.py, test infrastructure)
+from helpers import DATA, song  # noqa: E402
+import test_gpu_solver as ts  # noqa: E402
+
+KEYS = ts.KEYS
+
+
+def _stats(e):
+    e = np.asarray(e)
+    return {"n": int(e.size), "median": float(np.median(e)), "p99": float(np.percentile(e, 99)),
+            "max": float(e.max())}
+
+
+def case_bench():
+    md, g, o = ts._pair(dp, ref, "crossing_field", 64)
+    return _stats(ts._teacher_forced(md, g, o, 8, np.random.RandomState(21)))
+
+
+def case_coupled():
+    n, e = ts._replay(dp, ref, lambda st: st[:, 4] >= 10)
+    return _stats(e)
+
+
+def case_heavy():
+    n, e = ts._replay(dp, ref, lambda st: st[:, 3] > 40)
+    return _stats(e)
+
+
+def _drift_tf(kind, steps=200, n=8):
+    task = dp.TaskConfig()
+    seq = song(dp, "twinkle")
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
+    o = ref.OracleEnv(md, st, tc, n)
+    lo, hi = dp.model.action_spec(md)
+    rng = np.random.RandomState(12345)
+    trace = np.load(DATA / "twinkle_twinkle_actions.npy").astype(np.float32)
+    g.reset()
+    o.reset()
+    tf = []
+    for t in range(steps):
+        if kind == "trace":
+            a = np.repeat((lo + (trace[t % len(trace)] + 1) * 0.5 * (hi - lo)).astype(np.float32)[None], n, 0)
+        else:
+            a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
+        s = {k: v.cpu().numpy() for k, v in g.get_state().items()}
+        o.set_state({k: s[k] for k in KEYS})
+        g.step(torch.from_numpy(a).cuda())
+        o.step(a)
+        tf.append(np.abs(g.get_state()["qpos"].cpu().numpy() - o.get_state()["qpos"]).max(axis=1))
+    return _stats(np.concatenate(tf))
+
+
+def case_trace():
+    return _drift_tf("trace")
+
+
+def case_random():
+    return _drift_tf("random")
+
+
+def case_guren():
+    N = 4096
+    seq = song(dp, "guren")
+    task = dp.TaskConfig(trim_silence=True)
+    g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", canonical_actions=False)
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    lo, hi = (torch.tensor(x, device="cuda:0", dtype=torch.float32) for x in dp.model.action_spec(md))
+    gen = torch.Generator(device="cuda:0").manual_seed(8)
+    g.reset()
+    for _ in range(20):
+        u = torch.rand(N // 2, 45, device="cuda:0", generator=gen)
+        g.step(lo + torch.cat([u, u]) * (hi - lo))
+    idx = np.arange(0, N, N // 64)
+    o = ref.OracleEnv(md, st, tc, len(idx))
+    eqs = []
+    for _ in range(4):
+        sg = {k: v.cpu().numpy() for k, v in g.get_state().items()}
+        o.set_state({k: sg[k][idx] for k in KEYS})
+        a = lo + torch.rand(N, 45, device="cuda:0", generator=gen) * (hi - lo)
+        g.step(a)
+        o.step(a.cpu().numpy()[idx])
+        eqs.append(np.abs(g.get_state()["qpos"].cpu().numpy()[idx] - o.get_state()["qpos"]).max(axis=1))
+    return _stats(np.concatenate(eqs))
+
+
+CASES = {"bench": case_bench, "coupled": case_coupled, "heavy": case_heavy, "trace": case_trace,
+         "random": case_random, "guren": case_guren}
+
+if __name__ == "__main__":
+    ref.build()
+    lib = Path(os.environ.get("PIANOSIM_LIB", "libpianosim.so")).name
+    for name in sys.argv[1:] or list(CASES):
+        r = CASES[name]()
+        print(json.dumps({"lib": lib, "case": name, **r}), flush=True)
