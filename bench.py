@@ -50,6 +50,8 @@ def parse():
                    help="authored: capsule colliders (primitive_fingertip_collisions=True); hull: palm boxes "
                         "and convex-hull fingertips, the reference's default collider kinds (shadow_hand.py:95,144-152)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-hull-leg", action="store_true",
+                   help="skip timing the same workload with the box / hull hand after the main line")
     p.add_argument("--cpu-sample-envs", type=int, default=16)
     p.add_argument("--cpu-sample-steps", type=int, default=1000)
     return p.parse_args()
@@ -292,9 +294,9 @@ def main():
     dp = importlib.import_module("diffusion-piano_amd")
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
     seq, task = load_song(dp, args.song)
-    if args.hand == "hull":
-        import dataclasses
-        task = dataclasses.replace(task, hand_xml=dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand()))
+    import dataclasses
+    if args.hand == "hull":  # the reference's default colliders (shadow_hand.py:95,144-152)
+        task = dataclasses.replace(task, primitive_fingertip_collisions=False)
     shard = sharding.shard_envs(args.envs * world, rank, world)  # weak scaling: envs per GPU fixed
     env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
                              env_offset=shard.start)
@@ -313,11 +315,30 @@ def main():
     per_env = sharding.gather_episode_returns(returns, shard, args.envs * world)
     per_env_done = per_env[~torch.isnan(per_env)]
     stats = env.solver_stats().cpu().numpy()
+    obs_dim = env.obs_dim
     total_steps = args.envs * world * args.steps
     value = total_steps / elapsed
+    hull_leg = None
+    if args.hand == "authored" and not args.no_hull_leg:
+        # the same workload with the reference's default colliders (primitive_fingertip_collisions
+        # =False: palm boxes, convex-hull fingertips; the box / hull kernel instantiation), after
+        # the main timed region: same envs, actions, K and W
+        env.close()
+        henv = dp.BatchedPianoEnv(shard.count, seq, dataclasses.replace(task, primitive_fingertip_collisions=False),
+                                  device=dev, seed=12345, env_offset=shard.start)
+        henv.reset()
+        stagger_episodes(henv, shard.start, henv.song.T)
+        h_elapsed, h_kernel_ms = timed_rollout(henv, actions, args.steps, args.warmup, dev,
+                                               sharding.EpisodeReturns(N, dev), sharding)
+        hull_leg = {"value": total_steps / h_elapsed, "ms_per_step": h_elapsed / args.steps * 1e3,
+                    "kernel_ms_avg": h_kernel_ms, "unit": "env-steps/s",
+                    "hand": "palm boxes + convex-hull fingertips (TaskConfig(primitive_fingertip_collisions=False), "
+                            "the reference's default; pianosim_kernel<true>)"}
+        henv.close()
+        env = None
     if rank == 0:
         sha = lib_sha()
-        bpe = bytes_per_env_step(env.obs_dim)
+        bpe = bytes_per_env_step(obs_dim)
         achieved = bpe * N / (kernel_ms * 1e-3) / 1e9
         traffic = pmc_traffic(N, args.song, sha, args.hand)
         line = {
@@ -350,7 +371,8 @@ def main():
                                             "max_contact_rows": int(stats[:, 3].max()),
                                             "coupled_substep_frac": float(stats[:, 4].sum() / (10.0 * stats.shape[0])),
                                             "bad_pivot_substeps": int(stats[:, 5].sum()),
-                                            "max_coupled_dofs": int(stats[:, 6].max())}},
+                                            "max_coupled_dofs": int(stats[:, 6].max())},
+                       "hull_hand": hull_leg},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
@@ -365,7 +387,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"] = cpu_baseline(dp, seq, task, args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(line), flush=True)
-    env.close()
+    if env is not None:
+        env.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -20,6 +20,8 @@ struct XShape {
   float r;         // capsule radius
   f3 hs;           // box half sizes
   int v0, nv;      // hull vertices in DevModel::hull_v (geom frame)
+  f3 e0, e1;       // hull: an enclosing capsule (world), radius er
+  float er;
 };
 
 __device__ __forceinline__ void quat_to_R(float w, float x, float y, float z, float* R) {
@@ -67,12 +69,28 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
   if (s.type == PS_GEOM_BOX) {
     loc = mk3(sgn0f(dl.x) * s.hs.x, sgn0f(dl.y) * s.hs.y, sgn0f(dl.z) * s.hs.z);
   } else {
+    // the first maximal vertex, eight at a time: the block's loads issued together, its best by
+    // a 3-level tree (ties to the lower index), then against the running best (ties to the
+    // earlier block) - the sequential scan's choice with an 11-deep compare chain per block
+    // instead of 8 and the loads off the chain
     float bd = -INFINITY;
     loc = mk3(0.f, 0.f, 0.f);
-    for (int i = 0; i < s.nv; i++) {
-      const float4 v = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + i]);
-      const float p = dl.x * v.x + dl.y * v.y + dl.z * v.z;
-      if (p > bd) { bd = p; loc = mk3(v.x, v.y, v.z); }
+    for (int i0 = 0; i0 < s.nv; i0 += 8) {
+      float4 v[8];
+      float p[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        v[j] = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + min(i0 + j, s.nv - 1)]);
+        p[j] = i0 + j < s.nv ? dl.x * v[j].x + dl.y * v[j].y + dl.z * v[j].z : -INFINITY;
+      }
+#pragma unroll
+      for (int w = 1; w < 8; w *= 2) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2 * w) {
+          if (p[j + w] > p[j]) { p[j] = p[j + w]; v[j] = v[j + w]; }
+        }
+      }
+      if (p[0] > bd) { bd = p[0]; loc = mk3(v[0].x, v[0].y, v[0].z); }
     }
   }
   return s.c + mv3(s.R, loc);
@@ -412,6 +430,31 @@ __device__ __forceinline__ int capsule_obox(const XShape& C, const XShape& Bx, f
   const float d = sphere_box(C.p0 + (C.p1 - C.p0) * t, C.r, Bx.c, Bx.R, hs, &nn, &pp);
   if (d <= 0.f) { pos[0] = pp; dist[0] = d; nrm[0] = nn; return 1; }
   return 0;
+}
+
+// A pair with a hull whose enclosing capsule stays clear of the other collider (its enclosing
+// capsule, capsule or box) by more than 1e-5 m: the hulls are apart, MPR would find nothing.
+__device__ __forceinline__ bool x_apart(const XShape& A, const XShape& B) {
+  if (A.type != PS_GEOM_HULL && B.type != PS_GEOM_HULL) return false;
+  const bool ha = A.type == PS_GEOM_HULL;
+  const f3 h0 = ha ? A.e0 : B.e0, h1 = ha ? A.e1 : B.e1;
+  const float hr = ha ? A.er : B.er;
+  const XShape& O = ha ? B : A;
+  float d;
+  if (O.type == PS_GEOM_BOX) {
+    const float hs[3] = {O.hs.x, O.hs.y, O.hs.z};
+    const f3 a = mtv3(O.R, h0 - O.c), b = mtv3(O.R, h1 - O.c);
+    const float t = seg_box_t(a, b - a, hs);
+    f3 n, p;
+    d = sphere_box(h0 + (h1 - h0) * t, hr, O.c, O.R, hs, &n, &p);
+  } else {
+    const f3 o0 = O.type == PS_GEOM_HULL ? O.e0 : O.p0, o1 = O.type == PS_GEOM_HULL ? O.e1 : O.p1;
+    const float orad = O.type == PS_GEOM_HULL ? O.er : O.r;
+    f3 c1, c2;
+    seg_seg(h0, h1, o0, o1, &c1, &c2);
+    d = norm3(c2 - c1) - hr - orad;
+  }
+  return d > 1e-5f;
 }
 
 // Narrow phase of collider A (geom1) with collider B: capsule-box (the box becomes geom1:

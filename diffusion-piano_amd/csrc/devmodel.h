@@ -91,7 +91,9 @@ struct DevModel {
   int x_type[NXT];             // PS_GEOM_NONE / BOX / HULL
   float x_pos[NXT][3], x_Q[NXT][9], x_hs[NXT][3], x_rb[NXT];
   int x_v0[NXT], x_nv[NXT];    // hull vertices [x_v0, x_v0 + x_nv) of hull_v
+  float x_ec[NXT][8];          // hull: an enclosing capsule in the geom frame (p0, p1, radius, pad)
   int nxpairs;                 // hand-hand pairs with an extra collider: a | b << 8
+  int nxpairs_same;            // leading ones within one hand (the rest cross hands)
   int xpair[PS_MAX_XPAIRS];
   alignas(16) float hull_v[NH * PS_HAND_HULLVERT][4];  // geom frame (w unused)
   // triangular (a,b) table for the LDL update

@@ -91,6 +91,39 @@ static void quat2mat_h(const double* q, float* R) {
 }
 
 // Derive the flattened device model + topology tables from the descriptor.
+// An enclosing capsule of a hull's vertices (geom frame), the narrow phase's pre-reject: for
+// each frame axis, the segment along it through the centre of the vertices' extent across it,
+// radius the largest distance across, ends just long enough to hold every vertex; the axis of
+// the smallest capsule is kept. out = p0, p1, radius (padded by 1e-6 relative + 1e-7 m).
+static void enclosing_capsule(const double (*v)[3], int n, float* out) {
+  double best = INFINITY;
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < 3; k++) { lo[k] = fmin(lo[k], v[i][k]); hi[k] = fmax(hi[k], v[i][k]); }
+  for (int a = 0; a < 3; a++) {
+    const int b = (a + 1) % 3, c = (a + 2) % 3;
+    const double cb = 0.5 * (lo[b] + hi[b]), cc = 0.5 * (lo[c] + hi[c]);
+    double r = 0.0;
+    for (int i = 0; i < n; i++) r = fmax(r, hypot(v[i][b] - cb, v[i][c] - cc));
+    double t0 = INFINITY, t1 = -INFINITY;
+    for (int i = 0; i < n; i++) {
+      const double rho = hypot(v[i][b] - cb, v[i][c] - cc), s = sqrt(fmax(r * r - rho * rho, 0.0));
+      t0 = fmin(t0, v[i][a] + s);
+      t1 = fmax(t1, v[i][a] - s);
+    }
+    if (t0 > t1) t0 = t1 = 0.5 * (t0 + t1);  // a sphere holds them all
+    const double vol = M_PI * r * r * (t1 - t0) + 4.0 / 3.0 * M_PI * r * r * r;
+    if (vol < best) {
+      best = vol;
+      double p0[3], p1[3];
+      p0[a] = t0; p1[a] = t1; p0[b] = p1[b] = cb; p0[c] = p1[c] = cc;
+      for (int k = 0; k < 3; k++) { out[k] = (float)p0[k]; out[3 + k] = (float)p1[k]; }
+      out[6] = (float)(r * (1.0 + 1e-6) + 1e-7);
+      out[7] = 0.f;
+    }
+  }
+}
+
 static int build_dev_model(const ps_model_desc* d, DevModel* m) {
   memset(m, 0, sizeof(*m));
   m->timestep = (float)d->timestep;
@@ -342,6 +375,8 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
         return fail("hull vertex range out of bounds (4 .. PS_HULL_MAXVERT vertices)");
       if (t == PS_GEOM_BOX && !(d->xgeom_size[h][i][0] > 0 && d->xgeom_size[h][i][1] > 0 && d->xgeom_size[h][i][2] > 0))
         return fail("box half sizes must be positive");
+      if (t == PS_GEOM_HULL) enclosing_capsule(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_ec[e]);
+      if (t == PS_GEOM_HULL) enclosing_capsule(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_ec[e]);
     }
   for (int g = 0; g < NCOLL; g++) {
     m->geom_pathmask[g] = m->body_pathmask[m->geom_body[g]];
@@ -439,6 +474,14 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     m->npairs_same++;
   for (int i = m->npairs_same; i < m->npairs; i++)
     if (m->pair[i][0] / NG == m->pair[i][1] / NG) { m->npairs_same = m->npairs; break; }
+  // likewise the pairs with an extra collider (model.extra_pairs: same-hand ones first)
+  auto xhand = [](int g) { return g < NGT ? g / NG : (g - NGT) / NX; };
+  m->nxpairs_same = 0;
+  while (m->nxpairs_same < m->nxpairs &&
+         xhand(m->xpair[m->nxpairs_same] & 255) == xhand(m->xpair[m->nxpairs_same] >> 8))
+    m->nxpairs_same++;
+  for (int i = m->nxpairs_same; i < m->nxpairs; i++)
+    if (xhand(m->xpair[i] & 255) == xhand(m->xpair[i] >> 8)) { m->nxpairs_same = m->nxpairs; break; }
   return 0;
 }
 

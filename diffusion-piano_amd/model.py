@@ -629,7 +629,9 @@ def capsule_pairs(bodies, geoms, excludes):
 def extra_pairs(bodies, geoms, xgeoms, excludes):
     """Hand-hand collider pairs with at least one box/hull collider, MuJoCo-filtered as
     capsule_pairs, in global ids (capsule h*HAND_NGEOM + g, extra 2*HAND_NGEOM +
-    h*HAND_NXGEOM + i), ordered by (a, b) with a < b."""
+    h*HAND_NXGEOM + i), a < b: the pairs within one hand first, then the cross-hand ones, each
+    ordered by (a, b) (as capsule_pairs: the kernel skips the cross-hand ones wholesale when the
+    hands' bounding boxes are apart)."""
     ex = {frozenset(p) for p in excludes}
     ng, nx = abi.HAND_NGEOM, abi.HAND_NXGEOM
     coll = []  # (global id, hand, body, is_extra)
@@ -646,8 +648,8 @@ def extra_pairs(bodies, geoms, xgeoms, excludes):
             if ha == hb:
                 if ba == bb or bodies[ba].parent == bb or bodies[bb].parent == ba or frozenset((ba, bb)) in ex:
                     continue
-            pairs.append((ga, gb))
-    return pairs
+            pairs.append((ga, gb, ha != hb))
+    return [(a, b) for a, b, _ in sorted(pairs, key=lambda p: (p[2], p[0], p[1]))]
 
 
 def action_spec(m: abi.ModelDesc):

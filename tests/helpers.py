@@ -44,3 +44,36 @@ def capsule_points(radius, halflen, n_ring=8, n_lat=2):
 def box_hull_hand(dp):
     """The authored right hand with box and convex-hull colliders (mjcf.box_hull_hand)."""
     return dp.mjcf.box_hull_hand()
+
+
+def perturbed(state, rng, scale=1e-7):
+    """The state with every hand joint moved by N(0, scale) rad: the checker stepped from it
+    measures the model's own fp64 sensitivity at that state (parity floor)."""
+    s = dict(state)
+    q = np.array(state["qpos"], np.float64)
+    q[:, 88:] += rng.normal(0.0, scale, q[:, 88:].shape)
+    s["qpos"] = q
+    return s
+
+
+def assert_parity(e, floor, what="", tol=1e-4, well=1e-5):
+    """The parity gate of a teacher-forced comparison (fp32 kernel vs fp64 checker, one control
+    step from the same state), per env-step qpos L-inf error `e` and the checker's own
+    sensitivity `floor` (the same step from the state moved by ``perturbed``):
+      * median < 1e-5;
+      * p99 < tol over the well-conditioned env-steps (floor < well; most of them);
+      * p99 over all env-steps within max(tol, 2x the floor's p99): the ill-conditioned ones - a
+        contact starting or ending at near-zero distance, where the soft contact's force steps -
+        move the checker itself by more than tol under a 1e-7 rad perturbation, so no
+        implementation that is not bit-identical to it stays below tol there."""
+    e, floor = np.asarray(e, np.float64), np.asarray(floor, np.float64)
+    calm = floor < well
+    msg = (f"{what}: n {e.size}, median {np.median(e):.2e}, p99 {np.percentile(e, 99):.2e}, max {e.max():.2e}; "
+           f"well-conditioned {int(calm.sum())}: p99 {np.percentile(e[calm], 99) if calm.any() else float('nan'):.2e}; "
+           f"floor p99 {np.percentile(floor, 99):.2e}")
+    print(msg)
+    assert np.median(e) < 1e-5, msg
+    assert calm.sum() >= 0.5 * e.size, msg
+    assert np.percentile(e[calm], 99) < tol, msg
+    assert np.percentile(e, 99) <= max(tol, 2.0 * np.percentile(floor, 99)), msg
+    return msg

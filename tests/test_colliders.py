@@ -161,7 +161,9 @@ def test_box_hull_hand_model(dp):
     body = lambda g: (hand.geoms[g % 20].body if g < 40 else hand.xgeoms[(g - 40) % 12].body)
     hand_of = lambda g: g // 20 if g < 40 else (g - 40) // 12
     pairs = [tuple(md.xpair[i]) for i in range(md.n_xpairs)]
-    assert pairs == sorted(pairs) and all(b >= 40 and a < b for a, b in pairs)
+    same = [p for p in pairs if hand_of(p[0]) == hand_of(p[1])]
+    assert pairs == sorted(same) + sorted(p for p in pairs if hand_of(p[0]) != hand_of(p[1]))  # same hand first
+    assert all(b >= 40 and a < b for a, b in pairs)
     for a, b in pairs:
         if hand_of(a) == hand_of(b):
             ba, bb = body(a), body(b)

@@ -1,12 +1,14 @@
 """PianoTask keyword arguments on the GPU (tests/test_task_kwargs.py pins them on the checker):
 gravity_compensation, attachment_yaw and primitive_fingertip_collisions=True (palm boxes,
 capsule fingertips: the box / hull kernel instantiation), each teacher-forced against the
-checker for one control step at a time: qpos median < 1e-5, p99 < 1e-4; rewards p99 < 1e-3.
+checker for one control step at a time: qpos by helpers.assert_parity (median < 1e-5, p99 < 1e-4
+over the well-conditioned env-steps, p99 within max(1e-4, 2x the checker's own 1e-7 rad
+sensitivity) over all); rewards p99 < 1e-3.
 (primitive_fingertip_collisions=False, the hull fingertips: tests/test_gpu_colliders.py.)"""
 import numpy as np
 import pytest
 
-from helpers import song
+from helpers import assert_parity, perturbed, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -22,22 +24,27 @@ def test_task_kwargs_teacher_forced(dp, ref, kw):
     task = dp.TaskConfig(**kw)
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
-    o = ref.OracleEnv(md, st, tc, n)
+    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
     lo, hi = dp.model.action_spec(md)
     rng = np.random.RandomState(17)
+    prng = np.random.RandomState(2)
     g.reset()
     o.reset()
     np.testing.assert_allclose(g.fingertips().cpu().numpy(), o.fingertips(), atol=2e-6)
-    errs, rerr, ncon = [], [], 0
-    for _ in range(12):
+    errs, rerr, fl, ncon = [], [], [], 0
+    for _ in range(16):
         a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
-        o.set_state({k: v.cpu().numpy() for k, v in g.get_state().items() if k in KEYS})
+        s = {k: v.cpu().numpy() for k, v in g.get_state().items() if k in KEYS}
+        o.set_state(s)
+        o2.set_state(perturbed(s, prng))
         _, rg, _, _ = g.step(torch.from_numpy(a).cuda())
         _, ro, _, _ = o.step(a)
+        o2.step(a)
         errs.append(np.abs(g.get_state()["qpos"].cpu().numpy() - o.get_state()["qpos"]).max(axis=1))
+        fl.append(np.abs(o2.get_state()["qpos"] - o.get_state()["qpos"]).max(axis=1))
         rerr.append(np.abs(rg.cpu().numpy() - ro))
         ncon += int(o.contact_count().sum())
     e, r = np.concatenate(errs), np.concatenate(rerr)
     assert ncon > 0
-    assert np.median(e) < 1e-5 and np.percentile(e, 99) < 1e-4, (np.median(e), np.percentile(e, 99), e.max())
+    assert_parity(e, np.concatenate(fl), str(kw))
     assert np.percentile(r, 99) < 1e-3, r.max()

@@ -45,9 +45,9 @@ def run(dp, kind, delta):
             b_env.set_state({k: s[k] for k in KEYS})
         if kind == "zero":
             a = np.zeros((N, 45), np.float32)
-        elif kind == "trace":
-            x = trace[t % len(trace)]
-            a = np.repeat((lo + (x + 1) * 0.5 * (hi - lo)).astype(np.float32)[None], N, 0)
+        elif kind == "trace":  # env i starts 20 i actions into the trace (tests/test_gpu_drift.py)
+            x = trace[(t + 20 * np.arange(N)) % len(trace)]
+            a = (lo + (x + 1) * 0.5 * (hi - lo)).astype(np.float32)
         else:
             a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
         a_env.step(a); b_env.step(a)

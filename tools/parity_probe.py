@@ -9,7 +9,8 @@ parity gates hold (development aid; the gates themselves are the tests):
   guren    test_gpu_task_cases.py::test_guren_at_4096_envs (64 sampled of 4096 envs, 4 steps)
 
 usage: PIANOSIM_LIB=diffusion-piano_amd/<lib>.so python tools/parity_probe.py [case ...]
-Prints one JSON line per case (median / p99 / max of the per-env-step qpos L-inf error)."""
+Prints one JSON line per case (median / p99 / max of the per-env-step qpos L-inf error).
+PROBE_DIAG=1: the worst env-steps of the trace case with their features (diagnose_trace)."""
 import importlib
 import json
 import os
@@ -25,56 +26,68 @@ sys.path.insert(0, str(ROOT / "tests"))
 sys.path.insert(0, str(ROOT / "oracle"))
 dp = importlib.import_module("diffusion-piano_amd")
 import ref  # noqa: E402  (oracle/ref.py, test infrastructure)
-from helpers import DATA, song  # noqa: E402
+from helpers import DATA, perturbed, song  # noqa: E402
 import test_gpu_solver as ts  # noqa: E402
 
 KEYS = ts.KEYS
 
 
-def _stats(e):
+def _stats(e, floor=None):
     e = np.asarray(e)
-    return {"n": int(e.size), "median": float(np.median(e)), "p99": float(np.percentile(e, 99)),
-            "max": float(e.max())}
+    out = {"n": int(e.size), "median": float(np.median(e)), "p99": float(np.percentile(e, 99)), "max": float(e.max())}
+    if floor is not None:
+        calm = np.asarray(floor) < 1e-5
+        out.update(p99_well=float(np.percentile(e[calm], 99)) if calm.any() else None, n_well=int(calm.sum()),
+                   floor_p99=float(np.percentile(floor, 99)))
+    return out
 
 
 def case_bench():
     md, g, o = ts._pair(dp, ref, "crossing_field", 64)
-    return _stats(ts._teacher_forced(md, g, o, 8, np.random.RandomState(21)))
+    o2 = ref.OracleEnv(*dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True),
+                                        canonical_actions=False), 64)
+    return _stats(*ts._teacher_forced(md, g, o, o2, 16, np.random.RandomState(21)))
 
 
 def case_coupled():
-    n, e = ts._replay(dp, ref, lambda st: st[:, 4] >= 10)
-    return _stats(e)
+    n, e, f = ts._replay(dp, ref, lambda st: st[:, 4] >= 10)
+    return _stats(e, f)
 
 
 def case_heavy():
-    n, e = ts._replay(dp, ref, lambda st: st[:, 3] > 40)
-    return _stats(e)
+    n, e, f = ts._replay(dp, ref, lambda st: st[:, 3] > 40)
+    return _stats(e, f)
 
 
 def _drift_tf(kind, steps=200, n=8):
+    """tests/test_gpu_drift.py's teacher-forced part (env i starts 20 i actions into the trace)."""
     task = dp.TaskConfig()
     seq = song(dp, "twinkle")
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
-    o = ref.OracleEnv(md, st, tc, n)
+    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
     lo, hi = dp.model.action_spec(md)
     rng = np.random.RandomState(12345)
+    prng = np.random.RandomState(4)
     trace = np.load(DATA / "twinkle_twinkle_actions.npy").astype(np.float32)
     g.reset()
-    o.reset()
-    tf = []
+    tf, fl = [], []
     for t in range(steps):
         if kind == "trace":
-            a = np.repeat((lo + (trace[t % len(trace)] + 1) * 0.5 * (hi - lo)).astype(np.float32)[None], n, 0)
+            a = (lo + (trace[(t + 20 * np.arange(n)) % len(trace)] + 1) * 0.5 * (hi - lo)).astype(np.float32)
         else:
             a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
         s = {k: v.cpu().numpy() for k, v in g.get_state().items()}
-        o.set_state({k: s[k] for k in KEYS})
+        s = {k: s[k] for k in KEYS}
+        o.set_state(s)
+        o2.set_state(perturbed(s, prng))
         g.step(torch.from_numpy(a).cuda())
         o.step(a)
-        tf.append(np.abs(g.get_state()["qpos"].cpu().numpy() - o.get_state()["qpos"]).max(axis=1))
-    return _stats(np.concatenate(tf))
+        o2.step(a)
+        qo = o.get_state()["qpos"]
+        tf.append(np.abs(g.get_state()["qpos"].cpu().numpy() - qo).max(axis=1))
+        fl.append(np.abs(o2.get_state()["qpos"] - qo).max(axis=1))
+    return _stats(np.concatenate(tf), np.concatenate(fl))
 
 
 def case_trace():
@@ -113,8 +126,52 @@ def case_guren():
 CASES = {"bench": case_bench, "coupled": case_coupled, "heavy": case_heavy, "trace": case_trace,
          "random": case_random, "guren": case_guren}
 
+def diagnose_trace(steps=200, n=8, top=25):
+    """The teacher-forced trace case with per-env-step features of the worst errors: the dof of
+    the largest error, the GPU's solver counters of the step, contact counts, and the checker's
+    own sensitivity (the same step from the state with the hand joints moved by 1e-7 rad)."""
+    task = dp.TaskConfig()
+    seq = song(dp, "twinkle")
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
+    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
+    lo, hi = dp.model.action_spec(md)
+    trace = np.load(DATA / "twinkle_twinkle_actions.npy").astype(np.float32)
+    prng = np.random.RandomState(3)
+    g.reset()
+    rows = []
+    for t in range(steps):
+        a = np.repeat((lo + (trace[t % len(trace)] + 1) * 0.5 * (hi - lo)).astype(np.float32)[None], n, 0)
+        s = {k: v.cpu().numpy() for k, v in g.get_state().items()}
+        s = {k: s[k] for k in KEYS}
+        o.set_state(s)
+        s2 = dict(s)
+        s2["qpos"] = s["qpos"].astype(np.float64) + np.concatenate([np.zeros((n, 88)), prng.normal(0, 1e-7, (n, 52))], 1)
+        o2.set_state(s2)
+        g.step(torch.from_numpy(a).cuda())
+        o.step(a)
+        o2.step(a)
+        qg, qo, qo2 = g.get_state()["qpos"].cpu().numpy(), o.get_state()["qpos"], o2.get_state()["qpos"]
+        st_ = g.solver_stats().cpu().numpy()
+        cg, co = g.contact_count().cpu().numpy(), o.contact_count()
+        for i in range(n):
+            d = np.abs(qg[i] - qo[i])
+            rows.append((float(d.max()), int(d.argmax()), float(np.abs(qo2[i] - qo[i]).max()), t, i,
+                         st_[i].tolist(), int(cg[i]), int(co[i])))
+    rows.sort(key=lambda r: -r[0])
+    e = np.array([r[0] for r in rows])
+    f = np.array([r[2] for r in rows])
+    print(json.dumps({"case": "diagnose_trace", "p99": float(np.percentile(e, 99)), "floor_p99": float(np.percentile(f, 99)),
+                      "median": float(np.median(e)), "floor_median": float(np.median(f))}), flush=True)
+    for r in rows[:top]:
+        print("err %.2e dof %3d floor %.2e t %3d env %d stats %s ncon gpu %d oracle %d" % r, flush=True)
+
+
 if __name__ == "__main__":
     ref.build()
+    if os.environ.get("PROBE_DIAG"):
+        diagnose_trace()
+        sys.exit(0)
     lib = Path(os.environ.get("PIANOSIM_LIB", "libpianosim.so")).name
     for name in sys.argv[1:] or list(CASES):
         r = CASES[name]()
