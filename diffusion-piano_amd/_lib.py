@@ -17,6 +17,7 @@ EXPORTS = (
     "ps_reset", "ps_step", "ps_get_state", "ps_set_state", "ps_set_applied", "ps_reward_terms",
     "ps_fingertips", "ps_contact_count", "ps_musical_metrics", "ps_solver_stats", "ps_get_hand_offset",
     "ps_set_hand_offset", "ps_record_contacts", "ps_contacts", "ps_set_env_offset", "ps_warnings",
+    "ps_env_obs_dim", "ps_env_action_dim",
 )
 
 # Every entry point declared in include/pianorl.h.
@@ -72,7 +73,7 @@ def load() -> C.CDLL:
     if hasattr(L, "ps_set_env_offset"):
         L.ps_set_env_offset.argtypes = [vp, C.c_int64]
     for name, argc in (("ps_solver_stats", 3), ("ps_get_hand_offset", 4), ("ps_set_hand_offset", 3),
-                       ("ps_contacts", 3), ("ps_warnings", 3)):
+                       ("ps_contacts", 3), ("ps_warnings", 3), ("ps_env_obs_dim", 1), ("ps_env_action_dim", 1)):
         if hasattr(L, name):  # (absent from older builds loaded for A/B runs via PIANOSIM_LIB)
             getattr(L, name).argtypes = [vp] * argc
     for name in EXPORTS:

@@ -85,6 +85,8 @@ class ModelDesc(C.Structure):
         ("n_xpairs", i32), ("xpair", _arr(i32, MAX_XPAIRS, 2)),
         ("dof_frictionloss", _arr(d, NHAND, HAND_NDOF)), ("friction_solref", _arr(d, 2)),
         ("friction_solimp", _arr(d, 5)), ("hand_gravcomp", d),
+        ("dof_locked", _arr(i32, NHAND, HAND_NDOF)), ("n_obs_joints", _arr(i32, NHAND)),
+        ("act_column", _arr(i32, NHAND, HAND_NACT)), ("n_action", i32),
     ]
 
 
@@ -121,7 +123,15 @@ SOLVER_EXACT = SOLVER_NEWTON = 1
 HAND_POSITION_OFFSET = 0.05  # piano_with_shadow_hands.py:46
 
 
-def obs_dim(cfg: TaskCfg) -> int:
-    """goal (L+1)*89 + fingering 10 (if enabled) + piano/state 88 + sustain 1 + 2*26."""
+def obs_joints(md: "ModelDesc" = None):
+    """joints_pos entries per hand (26 each for the full hand)."""
+    if md is None:
+        return [HAND_NDOF] * NHAND
+    return [md.n_obs_joints[h] or HAND_NDOF for h in range(NHAND)]
+
+
+def obs_dim(cfg: TaskCfg, md: "ModelDesc" = None) -> int:
+    """goal (L+1)*89 + fingering 10 (if enabled) + piano/state 88 + sustain 1 + the joints_pos
+    entries of both hands (2*26 for the full hands)."""
     return (cfg.n_steps_lookahead + 1) * (NKEY + 1) + (10 if cfg.fingering_reward else 0) \
-        + NKEY + 1 + NHAND * HAND_NDOF
+        + NKEY + 1 + sum(obs_joints(md))

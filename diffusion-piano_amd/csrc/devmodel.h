@@ -70,7 +70,11 @@ struct DevModel {
   int ndepth, dep_start[MAXDEP + 1], dep_dof[NDT];
   int dof_act[NDT];          // actuator driving the dof (global index) or -1
   float dof_act_coef[NDT];
-  int obs_dof[NDT];          // joints_pos order -> global dof
+  int obs_dof[NDT];          // joints_pos order -> global dof (n_obsj entries: rh then lh)
+  int n_obsj;
+  uint64_t dof_lockmask;     // bit g: hand dof g is locked (a joint the reference's hand lacks)
+  int act_src[NU];           // column of actuator a in the caller's action row (-1: absent)
+  int n_action;              // action row width (the last column: sustain)
   // actuators, global a = h*NA + a
   int act_kind[NU], act_dof0[NU], act_dof1[NU], act_flim[NU];
   float act_c0[NU], act_c1[NU], act_kp[NU], act_clo[NU], act_chi[NU], act_flo[NU], act_fhi[NU];

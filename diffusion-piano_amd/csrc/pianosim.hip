@@ -36,7 +36,7 @@ static int fail(const std::string& s) {
   } while (0)
 
 struct ps_env {
-  int n, device, obs_dim;
+  int n, device, obs_dim, action_dim;
   int64_t env_offset;       // global id of local env 0 (Philox key of the per-env draws)
   int full_cpl;             // PIANOSIM_DEBUG_FULL_COUPLED: every coupled solve on the 28-column C block
   ps_task_cfg cfg;
@@ -223,9 +223,25 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       if (m->body_dof[B] < 0) m->body_dof[B] = g;
       else if (m->body_dof[B] + m->body_ndof[B] != g) return fail("dofs of a body must be contiguous");
       m->body_ndof[B]++;
-      m->obs_dof[g] = h * ND + d->dof_obs_order[h][j];
       m->dof_act[g] = -1;
+      if (d->dof_locked[h][j]) {  // a joint the reference's hand lacks: held at 0, no force / row
+        m->dof_lockmask |= 1ull << g;
+        m->dof_limited[g] = 0;
+        m->dof_floss[g] = 0.f;
+        m->dof_damp[g] = 0.f;
+      }
     }
+  m->n_obsj = 0;
+  for (int h = 0; h < NH; h++) {
+    const int nj = d->n_obs_joints[h] ? d->n_obs_joints[h] : ND;
+    if (nj < 0 || nj > ND) return fail("n_obs_joints out of range");
+    for (int j = 0; j < nj; j++) {
+      const int dof = d->dof_obs_order[h][j];
+      if (dof < 0 || dof >= ND) return fail("dof_obs_order out of range");
+      if (d->dof_locked[h][dof]) return fail("joints_pos lists a locked dof");
+      m->obs_dof[m->n_obsj++] = h * ND + dof;
+    }
+  }
   for (int B = 0; B < NBT; B++) {
     if (m->body_parent[B] >= 0 && m->body_ndof[B] != 1) return fail("non-root bodies need exactly one hinge");
     if (m->body_parent[B] >= 0 && m->dof_type[m->body_dof[B]] != 0) return fail("non-root dofs must be hinges");
@@ -277,7 +293,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
     uint64_t mask = 0;
     for (int x = B; x >= 0; x = m->body_parent[x])
       for (int j = 0; j < m->body_ndof[x]; j++) mask |= 1ull << (m->body_dof[x] + j);
-    m->body_pathmask[B] = mask;
+    m->body_pathmask[B] = mask & ~m->dof_lockmask;  // no Jacobian entry on a locked dof
   }
   int t = 0;
   for (int a = 1; a < MAXDEP; a++)
@@ -289,10 +305,18 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       for (int a = 1; a <= b; a++) { ta[c] = a; tb[c] = b; c++; }
     for (int i = 0; i < NTRI; i++) { m->tri_a[i] = ta[i]; m->tri_b[i] = tb[i]; }
   }
-  // actuators + tendons
+  // actuators + tendons; the caller's action row layout
+  m->n_action = d->n_action > 0 ? d->n_action : PS_NACTION;
+  if (m->n_action > PS_NACTION) return fail("n_action out of range");
+  uint64_t cols = 0;
   for (int h = 0; h < NH; h++)
     for (int a = 0; a < NA; a++) {
       int A = h * NA + a, tg = d->act_target[h][a];
+      const int col = d->n_action > 0 ? d->act_column[h][a] : A;
+      if (col < -1 || col >= m->n_action - 1) return fail("act_column out of range");
+      if (col >= 0 && ((cols >> col) & 1)) return fail("two actuators in one action column");
+      if (col >= 0) cols |= 1ull << col;
+      m->act_src[A] = col;
       m->act_kind[A] = d->act_kind[h][a];
       if (d->act_kind[h][a] == 0) {
         m->act_dof0[A] = h * ND + tg;
@@ -305,7 +329,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
         m->act_dof1[A] = h * ND + d->tendon_dof[h][tg][1];
         m->act_c1[A] = (float)d->tendon_coef[h][tg][1];
       }
-      m->act_kp[A] = (float)d->act_kp[h][a];
+      m->act_kp[A] = col >= 0 ? (float)d->act_kp[h][a] : 0.f;  // an absent actuator: no force
       m->act_clo[A] = (float)d->act_ctrlrange[h][a][0];
       m->act_chi[A] = (float)d->act_ctrlrange[h][a][1];
       m->act_flim[A] = d->act_forcelimited[h][a];
@@ -313,6 +337,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       m->act_fhi[A] = (float)d->act_forcerange[h][a][1];
       int dofs[2] = {m->act_dof0[A], m->act_dof1[A]};
       float cs[2] = {m->act_c0[A], m->act_c1[A]};
+      if (col < 0) continue;  // an absent actuator drives nothing
       for (int i = 0; i < (m->act_kind[A] == 1 ? 2 : 1); i++) {
         if (m->dof_act[dofs[i]] >= 0) return fail("a dof may be driven by at most one actuator");
         m->dof_act[dofs[i]] = A;
@@ -522,7 +547,8 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   E->n = n_envs;
   E->device = device;
   E->cfg = *cfg;
-  E->obs_dim = ps_obs_dim(cfg);
+  E->obs_dim = ps_obs_dim(cfg) - NH * ND + hm->n_obsj;  // the model's joints_pos entries
+  E->action_dim = hm->n_action;
   E->has_x = has_x;
   E->T = song->T;
   size_t N = (size_t)n_envs;
@@ -584,6 +610,9 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   *out = E;
   return 0;
 }
+
+int ps_env_obs_dim(const ps_env* E) { return E ? E->obs_dim : fail("null env"); }
+int ps_env_action_dim(const ps_env* E) { return E ? E->action_dim : fail("null env"); }
 
 void ps_destroy(ps_env* E) {
   if (!E) return;

@@ -22,7 +22,7 @@ import enum
 import math
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Any, Dict, NamedTuple, Optional, Union
+from typing import Any, Dict, NamedTuple, Optional, Tuple, Union
 
 import numpy as np
 
@@ -113,6 +113,11 @@ class TaskConfig:
     # distal colliders; False (the reference's default): palm boxes with convex-hull (mesh)
     # distal colliders, the step kernel's hull instantiation. Exclusive with hand_xml.
     primitive_fingertip_collisions: Optional[bool] = None
+    # THJ5, THJ1, LFJ5 and their actuators removed, THJ2 narrowed (shadow_hand.py:73-79,164-183):
+    # action 39, joints_pos 23 per hand
+    reduced_action_space: bool = False
+    # the forearm slides kept: a subset of ("forearm_tx", "forearm_ty") (shadow_hand.py:270-311)
+    forearm_dofs: Tuple[str, ...] = model_lib.FOREARM_DOFS
 
     def lookahead(self) -> int:
         if self.n_seconds_lookahead is not None:
@@ -150,7 +155,9 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
                                physics_timestep=cfg.physics_timestep,
                                hand_collisions=not cfg.disable_hand_collisions, hand=hand,
                                gravity_compensation=cfg.gravity_compensation,
-                               attachment_yaw=cfg.attachment_yaw)
+                               attachment_yaw=cfg.attachment_yaw,
+                               reduced_action_space=cfg.reduced_action_space,
+                               forearm_dofs=cfg.forearm_dofs)
     tc = abi.TaskCfg()
     tc.n_steps_lookahead = cfg.lookahead()
     tc.fingering_reward = int(not cfg.disable_fingering_reward and song.has_fingering)
@@ -168,9 +175,9 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
     return md, song, tc
 
 
-def obs_layout(tc: abi.TaskCfg) -> Dict[str, slice]:
+def obs_layout(tc: abi.TaskCfg, md: Optional[abi.ModelDesc] = None) -> Dict[str, slice]:
     """Observation keys in the order the reference driver concatenates them
-    (parallelized_base_v2.py:122-131)."""
+    (parallelized_base_v2.py:122-131); joints_pos as wide as the model's hands (``md``)."""
     out, o = {}, 0
     g = (tc.n_steps_lookahead + 1) * (abi.NKEY + 1)
     out["goal"] = slice(o, o + g); o += g
@@ -178,8 +185,9 @@ def obs_layout(tc: abi.TaskCfg) -> Dict[str, slice]:
         out["fingering"] = slice(o, o + 10); o += 10
     out["piano/state"] = slice(o, o + abi.NKEY); o += abi.NKEY
     out["piano/sustain_state"] = slice(o, o + 1); o += 1
-    out["rh_shadow_hand/joints_pos"] = slice(o, o + abi.HAND_NDOF); o += abi.HAND_NDOF
-    out["lh_shadow_hand/joints_pos"] = slice(o, o + abi.HAND_NDOF); o += abi.HAND_NDOF
+    nj = abi.obs_joints(md)
+    out["rh_shadow_hand/joints_pos"] = slice(o, o + nj[0]); o += nj[0]
+    out["lh_shadow_hand/joints_pos"] = slice(o, o + nj[1]); o += nj[1]
     return out
 
 
@@ -202,8 +210,9 @@ class BatchedPianoEnv:
         self.num_envs = int(num_envs)
         self.model_desc, self.song, self.task_cfg = compile_task(midi, self.task, canonical_actions)
         self.canonical_actions = canonical_actions
-        self.obs_dim = abi.obs_dim(self.task_cfg)
-        self.obs_slices = obs_layout(self.task_cfg)
+        self.obs_dim = abi.obs_dim(self.task_cfg, self.model_desc)
+        self.obs_slices = obs_layout(self.task_cfg, self.model_desc)
+        self.action_dim = model_lib.action_dim(self.model_desc)
         self.action_lo, self.action_hi = model_lib.action_spec(self.model_desc)
         L = _lib.load()
         sd = abi.SongDesc.from_tables(self.song)
@@ -214,6 +223,9 @@ class BatchedPianoEnv:
         _lib.check(L.ps_create(C.addressof(self.model_desc), C.addressof(sd), C.addressof(self.task_cfg),
                                self.num_envs, dev_index, seed, C.byref(h)))
         self._h = h
+        if hasattr(L, "ps_env_obs_dim") and (L.ps_env_obs_dim(h) != self.obs_dim or
+                                             L.ps_env_action_dim(h) != self.action_dim):
+            raise _lib.PianosimError("observation / action layout mismatch between the host and the library")
         if env_offset:
             _lib.check(L.ps_set_env_offset(h, int(env_offset)))
         N = self.num_envs
@@ -254,8 +266,8 @@ class BatchedPianoEnv:
     def step(self, action):
         torch = self._torch
         a = torch.as_tensor(action, device=self.device, dtype=torch.float32)
-        if a.shape != (self.num_envs, abi.NACTION):
-            raise ValueError(f"action must be [{self.num_envs}, {abi.NACTION}], got {tuple(a.shape)}")
+        if a.shape != (self.num_envs, self.action_dim):
+            raise ValueError(f"action must be [{self.num_envs}, {self.action_dim}], got {tuple(a.shape)}")
         a = a.contiguous()
         self._action = a  # keep alive until the kernel ran
         _lib.check(_lib.load().ps_step(self._h, a.data_ptr(), self.obs.data_ptr(), self.reward.data_ptr(),
@@ -380,10 +392,10 @@ class BatchedPianoEnv:
         return {k: Array((s.stop - s.start,), np.float64, k) for k, s in self.obs_slices.items()}
 
     def action_spec(self) -> BoundedArray:
+        n = self.action_dim
         if self.canonical_actions:
-            return BoundedArray((abi.NACTION,), np.float32, -np.ones(abi.NACTION, np.float32),
-                                np.ones(abi.NACTION, np.float32), "action")
-        return BoundedArray((abi.NACTION,), np.float32, self.action_lo.astype(np.float32),
+            return BoundedArray((n,), np.float32, -np.ones(n, np.float32), np.ones(n, np.float32), "action")
+        return BoundedArray((n,), np.float32, self.action_lo.astype(np.float32),
                             self.action_hi.astype(np.float32), "action")
 
 

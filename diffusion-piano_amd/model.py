@@ -68,6 +68,14 @@ CONTROL_TIMESTEP = 0.05   # tasks/base.py:31
 HAND_POSITIONS = [(0.4, 0.15, 0.13), (0.4, -0.15, 0.13)]  # right, left (tasks/base.py:34-37)
 HAND_QUAT = (-1.0, -1.0, 1.0, 1.0)
 ATTACHMENT_YAW = 0.0  # degrees (tasks/base.py:39 _ATTACHMENT_YAW)
+# PianoTask(reduced_action_space=True) (shadow_hand.py:51-57,164-183): these joints and their
+# actuators are removed, THJ2's range (and its actuator's ctrlrange) narrowed
+REDUCED_ACTION_SPACE_EXCLUDED = ("THJ5", "THJ1", "LFJ5")
+REDUCED_THUMB_RANGE = (0.0, 0.698132)
+# the forearm slides this hand models (shadow_hand.py:59-61 _DEFAULT_FOREARM_DOFS); the
+# reference's other forearm dofs (tz, roll, pitch, yaw) would need more dof slots than the
+# kernel's 26 per hand
+FOREARM_DOFS = ("forearm_tx", "forearm_ty")
 FINGERTIP_OFFSET = 0.026  # shadow_hand.py:81-82
 THUMBTIP_OFFSET = 0.0275
 FOREARM_KP = 300.0  # shadow_hand.py:41-52
@@ -386,7 +394,8 @@ def _subtree_mass(bodies, root):
 
 def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: float = PHYSICS_TIMESTEP,
                 hand_collisions: bool = True, hand: Optional[HandSpec] = None,
-                gravity_compensation: bool = False, attachment_yaw: float = ATTACHMENT_YAW) -> abi.ModelDesc:
+                gravity_compensation: bool = False, attachment_yaw: float = ATTACHMENT_YAW,
+                reduced_action_space: bool = False, forearm_dofs=FOREARM_DOFS) -> abi.ModelDesc:
     """Compile the scene into a ``ps_model_desc``.
 
     ``hand``: the right hand to use (``mjcf.load_hand`` of a user MJCF); default the authored
@@ -399,7 +408,20 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
     ``gravity_compensation`` (tasks/base.py:185-186): gravcomp = 1 on every hand body, a passive
     force cancelling the hands' gravity. ``attachment_yaw`` (degrees, tasks/base.py:174-181): the
     hand roots turned about world z by +yaw (right) / -yaw (left) before their quaternion.
+
+    ``reduced_action_space`` (shadow_hand.py:73-79,164-183) removes THJ5, THJ1 and LFJ5 with
+    their actuators and narrows THJ2 to (0, 0.698132); ``forearm_dofs`` (shadow_hand.py:270-311)
+    names the forearm slides the hand keeps, a subset of ("forearm_tx", "forearm_ty") in that
+    order. A removed joint keeps its dof slot, locked at 0 (``dof_locked``: no force, row or
+    Jacobian entry - MuJoCo's body without that joint), and leaves joints_pos and the action row
+    (``n_obs_joints``, ``act_column``, ``n_action``).
     """
+    forearm_dofs = tuple(forearm_dofs)
+    if any(f not in FOREARM_DOFS for f in forearm_dofs) or list(forearm_dofs) != [f for f in FOREARM_DOFS
+                                                                                   if f in forearm_dofs]:
+        raise ValueError(f"forearm_dofs must be a subset of {FOREARM_DOFS} in that order (this kernel's hand "
+                         f"has 26 dof slots: the reference's forearm_tz / roll / pitch / yaw do not fit), "
+                         f"got {forearm_dofs!r}")
     m = abi.ModelDesc()
     m.timestep = physics_timestep
     m.n_substeps = int(round(control_timestep / physics_timestep))
@@ -487,15 +509,38 @@ def build_model(control_timestep: float = CONTROL_TIMESTEP, physics_timestep: fl
         for t, (d2, d1) in enumerate(tendons):
             m.tendon_dof[h][t][:] = (d2, d1)
             m.tendon_coef[h][t][:] = tcoef[t]
+        # removed joints (reduced_action_space, forearm_dofs): locked dof slots
+        locked = [(reduced_action_space and any(dof.name.endswith(x) for x in REDUCED_ACTION_SPACE_EXCLUDED))
+                  or (dof.name in FOREARM_DOFS and dof.name not in forearm_dofs) for dof in dofs]
+        for j, dof in enumerate(dofs):
+            m.dof_locked[h][j] = int(locked[j])
+            if reduced_action_space and dof.name.endswith("THJ2"):
+                m.dof_range[h][j][:] = REDUCED_THUMB_RANGE
+        if any(locked):
+            oo = [j for j in obs_order if not locked[j]]
+            m.n_obs_joints[h] = len(oo)
+            for i in range(abi.HAND_NDOF):
+                m.dof_obs_order[h][i] = oo[i] if i < len(oo) else 0
         for a, (kind, target, kp, cr, fr) in enumerate(acts):
             m.act_kind[h][a] = kind
             m.act_target[h][a] = target
             m.act_kp[h][a] = kp
             if kind == 0 and dofs[target].name == "forearm_tx":
                 cr = (-PIANO_LENGTH / 2 - y, PIANO_LENGTH / 2 - y)
+            if kind == 0 and reduced_action_space and dofs[target].name.endswith("THJ2"):
+                cr = REDUCED_THUMB_RANGE
             m.act_ctrlrange[h][a][:] = cr
             m.act_forcelimited[h][a] = 0 if fr is None else 1
             m.act_forcerange[h][a][:] = (0.0, 0.0) if fr is None else fr
+    if any(m.dof_locked[h][j] for h in range(abi.NHAND) for j in range(abi.HAND_NDOF)):
+        # the action row: each hand's actuators on kept joints in order, then sustain
+        col = 0
+        for h in range(abi.NHAND):
+            for a, (kind, target, *_) in enumerate(acts):
+                present = kind == 1 or not m.dof_locked[h][target]
+                m.act_column[h][a] = col if present else -1
+                col += present
+        m.n_action = col + 1
     xgeoms = spec.xgeoms or []
     if len(geoms) > abi.HAND_NGEOM or len(xgeoms) > abi.HAND_NXGEOM:
         raise ValueError(f"at most {abi.HAND_NGEOM} capsule and {abi.HAND_NXGEOM} box/hull colliders per hand "
@@ -595,11 +640,13 @@ def set_const(m: abi.ModelDesc) -> None:
             Il = np.array([[I6[0], I6[3], I6[4]], [I6[3], I6[1], I6[5]], [I6[4], I6[5], I6[2]]])
             Iw = R[b] @ Il @ R[b].T
             M += m.body_mass[h][b] * Jp[b].T @ Jp[b] + Jr[b].T @ Iw @ Jr[b]
-        Minv = np.linalg.inv(M)
+        free = [j for j in range(nd) if not m.dof_locked[h][j]]  # a removed joint: not in M
+        Minv = np.zeros((nd, nd))
+        Minv[np.ix_(free, free)] = np.linalg.inv(M[np.ix_(free, free)])
         for b in range(nb):
             m.body_invweight[h][b] = float(np.trace(Jp[b] @ Minv @ Jp[b].T)) / 3.0
         for j in range(nd):
-            m.dof_invweight[h][j] = float(Minv[j, j])
+            m.dof_invweight[h][j] = float(Minv[j, j]) if j in free else 1.0
 
 
 def capsule_pairs(bodies, geoms, excludes):
@@ -652,14 +699,27 @@ def extra_pairs(bodies, geoms, xgeoms, excludes):
     return [(a, b) for a, b, _ in sorted(pairs, key=lambda p: (p[2], p[0], p[1]))]
 
 
+def action_dim(m: abi.ModelDesc) -> int:
+    """The action row width: 45 for the full hands; fewer without some joints (n_action)."""
+    return m.n_action if m.n_action > 0 else abi.NACTION
+
+
+def action_columns(m: abi.ModelDesc):
+    """[(hand, actuator, column)] of the actuators in the action row."""
+    return [(h, a, m.act_column[h][a] if m.n_action > 0 else h * abi.HAND_NACT + a)
+            for h in range(abi.NHAND) for a in range(abi.HAND_NACT)
+            if m.n_action <= 0 or m.act_column[h][a] >= 0]
+
+
 def action_spec(m: abi.ModelDesc):
-    """Action bounds [45]: right hand 22, left hand 22, sustain [0, 1]
-    (piano_with_shadow_hands.py:226-237)."""
-    lo = np.zeros(abi.NACTION)
-    hi = np.zeros(abi.NACTION)
-    for h in range(abi.NHAND):
-        for a in range(abi.HAND_NACT):
-            lo[h * abi.HAND_NACT + a] = m.act_ctrlrange[h][a][0]
-            hi[h * abi.HAND_NACT + a] = m.act_ctrlrange[h][a][1]
+    """Action bounds [action_dim]: right hand 22, left hand 22, sustain [0, 1]
+    (piano_with_shadow_hands.py:226-237); without the removed actuators when the model lacks
+    some joints (reduced_action_space, forearm_dofs)."""
+    n = action_dim(m)
+    lo = np.zeros(n)
+    hi = np.zeros(n)
+    for h, a, c in action_columns(m):
+        lo[c] = m.act_ctrlrange[h][a][0]
+        hi[c] = m.act_ctrlrange[h][a][1]
     lo[-1], hi[-1] = 0.0, 1.0
     return lo, hi

@@ -171,6 +171,18 @@ typedef struct {
    * tasks/base.py:185-186: mujoco_utils.physics_utils.compensate_gravity sets 1): a passive force
    * -gravcomp m g at each hand body's COM, i.e. the hands feel (1 - gravcomp) of the gravity */
   double hand_gravcomp;
+  /* Joints the reference's hand does not have - PianoTask(reduced_action_space=True) removes
+   * THJ5, THJ1 and LFJ5 (shadow_hand.py:73-79,164-183), forearm_dofs without forearm_tx /
+   * forearm_ty leaves that slide out (shadow_hand.py:270-311): the dof slot stays in qpos / qvel,
+   * held at 0 with no force, no constraint row and no Jacobian entry, so its child body rides its
+   * parent rigidly at the joint's zero - MuJoCo's body without that joint. */
+  int32_t dof_locked[PS_NHAND][PS_HAND_NDOF];
+  int32_t n_obs_joints[PS_NHAND];  /* joints_pos entries: dof_obs_order[h][0 .. n) (0: PS_HAND_NDOF) */
+  /* The caller's action row: n_action columns, the last one the sustain pedal; act_column[h][a]
+   * = actuator a's column, -1 when the reference has no such actuator (no force). n_action = 0:
+   * the full PS_NACTION layout (actuator h * PS_HAND_NACT + a in that column). */
+  int32_t act_column[PS_NHAND][PS_HAND_NACT];
+  int32_t n_action;
 } ps_model_desc;
 
 /* Song tables: NoteTrajectory in dense form (music.py:SongTables). */
@@ -264,19 +276,24 @@ typedef struct ps_env ps_env;
 
 const char* ps_last_error(void);
 int ps_version(void);
-int ps_obs_dim(const ps_task_cfg* cfg);
+int ps_obs_dim(const ps_task_cfg* cfg);  /* the full hand (n_obs_joints = PS_HAND_NDOF) */
 /* sizeof(ps_model_desc), for host-side layout checks. */
 int ps_model_desc_size(void);
 
 int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_task_cfg* cfg,
               int n_envs, int device, uint64_t seed, ps_env** out);
 void ps_destroy(ps_env* env);
+/* The handle's observation width and action row width (the model's joints_pos entries and
+ * actuators: the reference's VecEnv shapes, parallelized_base_v2.py:41-51). */
+int ps_env_obs_dim(const ps_env* env);
+int ps_env_action_dim(const ps_env* env);
 
 /* Resets envs (all when env_mask == NULL, else where env_mask[i] != 0; device u8[N])
  * and writes their first observation into obs[N][obs_dim]. */
 int ps_reset(ps_env* env, const uint8_t* env_mask, float* obs, void* stream);
 
-/* action[N][45] in spec units, or canonical [-1,1] units when cfg.canonical_actions. Envs whose
+/* action[N][ps_env_action_dim] (45 for the full hand) in spec units, or canonical [-1,1] units
+ * when cfg.canonical_actions. Envs whose
  * previous step was LAST are reset instead and report PS_FIRST (reward 0, discount 1). */
 int ps_step(ps_env* env, const float* action, float* obs, float* reward, float* discount,
             uint8_t* step_type, void* stream);

@@ -60,6 +60,16 @@ static inline v3 crs(v3 a, v3 b) {
 }
 static inline double nrm(v3 a) { return sqrt(dot(a, a)); }
 static inline double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+/* the model's action row and joints_pos layout (ps_model_desc n_action / act_column /
+ * n_obs_joints; 0 = the full hand) */
+static inline int n_action(const ps_model_desc* d) { return d->n_action > 0 ? d->n_action : PS_NACTION; }
+static inline int act_col(const ps_model_desc* d, int h, int a) {
+  return d->n_action > 0 ? d->act_column[h][a] : h * PS_HAND_NACT + a;
+}
+static inline int act_present(const ps_model_desc* d, int h, int a) { return act_col(d, h, a) >= 0; }
+static inline int n_obs_joints(const ps_model_desc* d, int h) {
+  return d->n_obs_joints[h] ? d->n_obs_joints[h] : PS_HAND_NDOF;
+}
 
 typedef struct { double m[9]; } m3;  /* row-major */
 static inline v3 mv(m3 R, v3 a) {
@@ -350,6 +360,12 @@ static void dynamics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       }
       E->M[h][i][i] += d->dof_armature[h][i];
     }
+    /* a locked dof (a joint the reference's hand lacks): identity row and column */
+    for (int i = 0; i < ND; i++)
+      if (d->dof_locked[h][i]) {
+        for (int j = 0; j < ND; j++) E->M[h][i][j] = E->M[h][j][i] = 0.0;
+        E->M[h][i][i] = 1.0;
+      }
     /* bias forces: RNE, gravity as base acceleration */
     v3 w[NB], al[NB], vo[NB], ac[NB], F[NB], N[NB];
     for (int b = 0; b < NB; b++) {
@@ -414,7 +430,7 @@ static void dynamics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       if (d->act_kind[h][a] == 0) len = qh[tg];
       else len = d->tendon_coef[h][tg][0] * qh[d->tendon_dof[h][tg][0]] + d->tendon_coef[h][tg][1] * qh[d->tendon_dof[h][tg][1]];
       double c = clampd(E->ctrl[h * NA + a], d->act_ctrlrange[h][a][0], d->act_ctrlrange[h][a][1]);
-      double f = d->act_kp[h][a] * (c - len);
+      double f = act_present(d, h, a) ? d->act_kp[h][a] * (c - len) : 0.0;
       if (d->act_forcelimited[h][a]) f = clampd(f, d->act_forcerange[h][a][0], d->act_forcerange[h][a][1]);
       E->act_force[h * NA + a] = f;
       if (d->act_kind[h][a] == 0) E->actfrc[NK + h * ND + tg] += f;
@@ -1123,6 +1139,7 @@ static void jac_point(const model* m, const envdata* E, int h, int b, v3 p, v3 u
   const ps_model_desc* d = &m->d;
   for (int bb = b; bb >= 0; bb = d->body_parent[h][bb]) {
     for (int j = m->body_dofadr[h][bb]; j >= 0 && j < m->body_dofadr[h][bb] + m->body_dofnum[h][bb]; j++) {
+      if (d->dof_locked[h][j]) continue;  /* a joint the reference's hand lacks */
       double val = d->dof_type[h][j] == 0 ? dot(u, crs(E->axis[h][j], sub(p, E->o[h][bb]))) : dot(u, E->axis[h][j]);
       J[NK + h * ND + j] += sgn * val;
     }
@@ -1451,6 +1468,10 @@ static int bad_vec(const double* x, int n) {
 static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
   const ps_model_desc* d = &m->d;
   const double h_t = d->timestep;
+  /* a locked dof stays at its joint zero */
+  for (int h = 0; h < NH; h++)
+    for (int j = 0; j < ND; j++)
+      if (d->dof_locked[h][j]) E->q[NK + h * ND + j] = E->v[NK + h * ND + j] = 0.0;
   /* mj_checkPos, mj_checkVel (mj_step1) */
   if (bad_vec(E->q, NV)) reset_physics(E, PS_WARN_BADQPOS);
   if (bad_vec(E->v, NV)) reset_physics(E, PS_WARN_BADQVEL);
@@ -1461,12 +1482,16 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     for (int h = 0; h < NH; h++) {
       memcpy(E->Mfull[h], E->M[h], sizeof(E->M[h]));
       memcpy(E->Mh[h], E->M[h], sizeof(E->M[h]));
-      for (int j = 0; j < ND; j++) E->Mh[h][j][j] += h_t * d->dof_damping[h][j];
+      for (int j = 0; j < ND; j++)
+        if (!d->dof_locked[h][j]) E->Mh[h][j][j] += h_t * d->dof_damping[h][j];
       factor(m, h, E->M[h], E->D[h]);
       factor(m, h, E->Mh[h], E->Dh[h]);
     }
     double fsmooth[NV], qacc_smooth[NV];
     for (int i = 0; i < NV; i++) fsmooth[i] = E->passive[i] + E->actfrc[i] + E->applied[i] - E->bias[i];
+    for (int h = 0; h < NH; h++)
+      for (int j = 0; j < ND; j++)
+        if (d->dof_locked[h][j]) fsmooth[NK + h * ND + j] = 0.0;
     solve_full(m, E, 0, fsmooth, qacc_smooth);
 
     /* rows: friction loss (hand dofs), hand limits, key limits (keys touched by a contact are
@@ -1479,7 +1504,7 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
     int nr = 0;
     for (int h = 0; h < NH; h++)
       for (int j = 0; j < ND; j++) {
-        if (!(d->dof_frictionloss[h][j] > 0.0)) continue;
+        if (!(d->dof_frictionloss[h][j] > 0.0) || d->dof_locked[h][j]) continue;
         row* r = &g_rows[nr++];
         memset(r->J, 0, sizeof(r->J));
         r->J[NK + h * ND + j] = 1.0;
@@ -1490,7 +1515,7 @@ static void step_physics(const model* m, const ps_task_cfg* cfg, envdata* E) {
       }
     for (int h = 0; h < NH; h++)
       for (int j = 0; j < ND; j++) {
-        if (!d->dof_limited[h][j]) continue;
+        if (!d->dof_limited[h][j] || d->dof_locked[h][j]) continue;
         double q = E->q[NK + h * ND + j];
         for (int side = 0; side < 2; side++) {
           double dist = side == 0 ? q - d->dof_range[h][j][0] : d->dof_range[h][j][1] - q;
@@ -1681,7 +1706,7 @@ static void write_obs(ref_env* R, envdata* E, float* obs, int t_obs) {
   for (int k = 0; k < NK; k++) obs[o++] = (float)E->norm_state[k];
   obs[o++] = (float)E->sustain;
   for (int h = 0; h < NH; h++)
-    for (int j = 0; j < ND; j++) obs[o++] = (float)E->q[NK + h * ND + d->dof_obs_order[h][j]];
+    for (int j = 0; j < n_obs_joints(d, h); j++) obs[o++] = (float)E->q[NK + h * ND + d->dof_obs_order[h][j]];
 }
 
 static void key_state(const model* m, envdata* E) {
@@ -1740,8 +1765,13 @@ static void control_step(ref_env* R, envdata* E, const float* a, float* obs, flo
     *rew = 0.0f; *disc = 1.0f; *st = PS_FIRST;
     return;
   }
-  for (int i = 0; i < PS_NU; i++) E->ctrl[i] = a[i];
-  E->sustain = a[PS_NU];
+  /* the caller's row: actuator columns (an absent actuator: ctrl 0), then the sustain pedal */
+  for (int h = 0; h < NH; h++)
+    for (int u = 0; u < NA; u++) {
+      const int col = act_col(d, h, u);
+      E->ctrl[h * NA + u] = col >= 0 ? a[col] : 0.0;
+    }
+  E->sustain = a[n_action(d) - 1];
   for (int s = 0; s < d->n_substeps; s++) step_physics(m, &R->cfg, E);
   kinematics(m, E);   /* mj_step1 at the final state (legacy_step) */
   collide(m, &R->cfg, E);
@@ -1890,8 +1920,10 @@ void ref_destroy(ref_env* R) {
 }
 
 int ref_obs_dim(const ref_env* R) {
-  return (R->cfg.n_steps_lookahead + 1) * (NK + 1) + (R->cfg.fingering_reward ? 10 : 0) + NK + 1 + NH * ND;
+  return (R->cfg.n_steps_lookahead + 1) * (NK + 1) + (R->cfg.fingering_reward ? 10 : 0) + NK + 1 +
+         n_obs_joints(&R->m.d, 0) + n_obs_joints(&R->m.d, 1);
 }
+int ref_action_dim(const ref_env* R) { return n_action(&R->m.d); }
 
 void ref_reset(ref_env* R, const uint8_t* mask, float* obs) {
   int od = ref_obs_dim(R);
@@ -1902,7 +1934,7 @@ void ref_reset(ref_env* R, const uint8_t* mask, float* obs) {
 void ref_step(ref_env* R, const float* action, float* obs, float* rew, float* disc, uint8_t* st) {
   int od = ref_obs_dim(R);
   for (int i = 0; i < R->n; i++)
-    control_step(R, &R->e[i], action + (size_t)i * PS_NACTION, obs + (size_t)i * od, rew + i, disc + i, st + i);
+    control_step(R, &R->e[i], action + (size_t)i * n_action(&R->m.d), obs + (size_t)i * od, rew + i, disc + i, st + i);
 }
 
 /* The all-cores CPU baseline: the same per-env step, envs spread over
@@ -1912,7 +1944,7 @@ void ref_step_threads(ref_env* R, const float* action, float* obs, float* rew, f
   int od = ref_obs_dim(R);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
   for (int i = 0; i < R->n; i++)
-    control_step(R, &R->e[i], action + (size_t)i * PS_NACTION, obs + (size_t)i * od, rew + i, disc + i, st + i);
+    control_step(R, &R->e[i], action + (size_t)i * n_action(&R->m.d), obs + (size_t)i * od, rew + i, disc + i, st + i);
 }
 
 void ref_get_state(const ref_env* R, double* q, double* v, double* qacc_ws, double* ctrl, double* sustain,

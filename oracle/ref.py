@@ -36,6 +36,7 @@ def _bind(L):
     L.ref_create.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     L.ref_destroy.argtypes = [C.c_void_p]
     L.ref_obs_dim.argtypes = [C.c_void_p]
+    L.ref_action_dim.argtypes = [C.c_void_p]
     L.ref_reset.argtypes = [C.c_void_p, C.c_void_p, _f32p]
     L.ref_step.argtypes = [C.c_void_p, _f32p, _f32p, _f32p, _f32p, _u8p]
     L.ref_step_threads.argtypes = [C.c_void_p, _f32p, _f32p, _f32p, _f32p, _u8p, C.c_int]
@@ -159,6 +160,7 @@ class OracleEnv:
         self.n = n_envs
         self._h = self._L.ref_create(C.addressof(model_desc), C.addressof(sd), C.addressof(cfg), n_envs)
         self.obs_dim = self._L.ref_obs_dim(self._h)
+        self.action_dim = self._L.ref_action_dim(self._h)
         self._L.ref_set_seed(self._h, seed)
         self._L.ref_set_env_offset(self._h, env_offset)
 
@@ -176,7 +178,7 @@ class OracleEnv:
     def step(self, action, threads: int = 1):
         """One control step of every env; ``threads > 1`` spreads the envs over OpenMP
         threads (the all-cores CPU baseline; results identical to the serial loop)."""
-        a = np.ascontiguousarray(action, np.float32).reshape(self.n, self.NACTION)
+        a = np.ascontiguousarray(action, np.float32).reshape(self.n, self.action_dim)
         obs = np.zeros((self.n, self.obs_dim), np.float32)
         rew = np.zeros(self.n, np.float32)
         disc = np.zeros(self.n, np.float32)

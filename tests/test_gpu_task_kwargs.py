@@ -1,6 +1,7 @@
 """PianoTask keyword arguments on the GPU (tests/test_task_kwargs.py pins them on the checker):
-gravity_compensation, attachment_yaw and primitive_fingertip_collisions=True (palm boxes,
-capsule fingertips: the box / hull kernel instantiation), each teacher-forced against the
+gravity_compensation, attachment_yaw, primitive_fingertip_collisions=True (palm boxes,
+capsule fingertips: the box / hull kernel instantiation), reduced_action_space (39-wide actions,
+three joints locked) and forearm_dofs=("forearm_tx",), each teacher-forced against the
 checker for one control step at a time: qpos by helpers.assert_parity (median < 1e-5, p99 < 1e-4
 over the well-conditioned env-steps, p99 within max(1e-4, 2x the checker's own 1e-7 rad
 sensitivity) over all); rewards p99 < 1e-3.
@@ -17,7 +18,9 @@ KEYS = ("qpos", "qvel", "qacc_ws", "ctrl", "sustain", "t_idx", "last")
 
 
 @pytest.mark.parametrize("kw", [dict(gravity_compensation=True), dict(attachment_yaw=15.0),
-                                dict(primitive_fingertip_collisions=True)], ids=["gravcomp", "yaw", "primitive"])
+                                dict(primitive_fingertip_collisions=True), dict(reduced_action_space=True),
+                                dict(forearm_dofs=("forearm_tx",))],
+                         ids=["gravcomp", "yaw", "primitive", "reduced", "forearm_tx"])
 def test_task_kwargs_teacher_forced(dp, ref, kw):
     n = 32
     seq = song(dp, "twinkle")
@@ -33,7 +36,7 @@ def test_task_kwargs_teacher_forced(dp, ref, kw):
     np.testing.assert_allclose(g.fingertips().cpu().numpy(), o.fingertips(), atol=2e-6)
     errs, rerr, fl, ncon = [], [], [], 0
     for _ in range(16):
-        a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
+        a = rng.uniform(lo, hi, (n, len(lo))).astype(np.float32)
         s = {k: v.cpu().numpy() for k, v in g.get_state().items() if k in KEYS}
         o.set_state(s)
         o2.set_state(perturbed(s, prng))
@@ -46,5 +49,9 @@ def test_task_kwargs_teacher_forced(dp, ref, kw):
         ncon += int(o.contact_count().sum())
     e, r = np.concatenate(errs), np.concatenate(rerr)
     assert ncon > 0
+    if md.n_action:  # removed joints stay at their zero, as in the oracle
+        q = g.get_state()["qpos"].cpu().numpy()
+        locked = [88 + 26 * h + j for h in range(2) for j in range(26) if md.dof_locked[h][j]]
+        assert locked and np.abs(q[:, locked]).max() == 0.0
     assert_parity(e, np.concatenate(fl), str(kw))
     assert np.percentile(r, 99) < 1e-3, r.max()
