@@ -22,6 +22,8 @@ struct XShape {
   int v0, nv;      // hull vertices in DevModel::hull_v (geom frame)
   f3 e0, e1;       // hull: an enclosing capsule (world), radius er
   float er;
+  const float* hx;  // hull: the LDS copy of DevModel::hl (x; y at hx + HL_MAX; z at hz; v0 indexes
+  const float* hz;  // it), or nullptr: DevModel::hull_v
 };
 
 __device__ __forceinline__ void quat_to_R(float w, float x, float y, float z, float* R) {
@@ -68,6 +70,24 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
   f3 loc;
   if (s.type == PS_GEOM_BOX) {
     loc = mk3(sgn0f(dl.x) * s.hs.x, sgn0f(dl.y) * s.hs.y, sgn0f(dl.z) * s.hs.z);
+  } else if (s.hx) {
+    // the first maximal vertex from the LDS copy, four at a time (by coordinate, one 16-byte read
+    // per coordinate; a hull starts 4-aligned, its padding repeats the last vertex): the block's
+    // best by a 2-level tree (ties to the lower index), then against the running best
+    float bd = -INFINITY;
+    loc = mk3(0.f, 0.f, 0.f);
+    for (int i0 = 0; i0 < s.nv; i0 += 4) {
+      const float4 X = *reinterpret_cast<const float4*>(s.hx + s.v0 + i0);
+      const float4 Y = *reinterpret_cast<const float4*>(s.hx + HL_MAX + s.v0 + i0);
+      const float4 Z = *reinterpret_cast<const float4*>(s.hz + s.v0 + i0);
+      float p[4] = {dl.x * X.x + dl.y * Y.x + dl.z * Z.x, dl.x * X.y + dl.y * Y.y + dl.z * Z.y,
+                    dl.x * X.z + dl.y * Y.z + dl.z * Z.z, dl.x * X.w + dl.y * Y.w + dl.z * Z.w};
+      f3 v[4] = {mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(X.w, Y.w, Z.w)};
+      if (p[1] > p[0]) { p[0] = p[1]; v[0] = v[1]; }
+      if (p[3] > p[2]) { p[2] = p[3]; v[2] = v[3]; }
+      if (p[2] > p[0]) { p[0] = p[2]; v[0] = v[2]; }
+      if (p[0] > bd) { bd = p[0]; loc = v[0]; }
+    }
   } else {
     // the first maximal vertex, eight at a time: the block's loads issued together, its best by
     // a 3-level tree (ties to the lower index), then against the running best (ties to the
@@ -166,7 +186,7 @@ __device__ __forceinline__ f3 mpr_pos(const MprPt& p0, const MprPt& p1, const Mp
 }
 // 1: penetrating (depth >= 0, normal A -> B, contact point); 0: apart
 __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
-                                               float* depth, f3* n, f3* pos) {
+                                               float* depth, f3* n, f3* pos, int* its = nullptr) {
   MprPt p0, p1, p2, p3;
   p0.a = A.c; p0.b = B.c; p0.v = A.c - B.c;
   if (p0.v.x == 0.f && p0.v.y == 0.f && p0.v.z == 0.f) p0.v.x += 10.f * MPR_EPSF;
@@ -188,6 +208,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
   dir = nrmz3(cross3(p1.v - p0.v, p2.v - p0.v));
   if (dot3(dir, p0.v) > 0.f) { const MprPt t = p1; p1 = p2; p2 = t; dir = dir * -1.f; }
   for (int it = 0;; it++) {
+    if (its) ++*its;  // (timing build: support calls of the refinement)
     if (it > 4 * MPR_MAXITF) return 0;
     p3 = mpr_sup(m, A, B, dir);
     dt = dot3(p3.v, dir);
@@ -203,6 +224,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
     dir = nrmz3(cross3(p1.v - p0.v, p2.v - p0.v));
   }
   for (int it = 0;; it++) {
+    if (its) ++*its;  // (timing build: support calls of the refinement)
     if (it > 4 * MPR_MAXITF) return 0;
     dir = portal_dir(p1, p2, p3);
     dt = dot3(p1.v, dir);
@@ -213,6 +235,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
     expand_portal(p0, p1, p2, p3, v4);
   }
   for (int it = 0;; it++) {
+    if (its) ++*its;  // (timing build: support calls of the refinement)
     dir = portal_dir(p1, p2, p3);
     const MprPt v4 = mpr_sup(m, A, B, dir);
     if (portal_reach_tol(p1, p2, p3, v4, dir) || it > MPR_MAXITF) {
@@ -461,7 +484,8 @@ __device__ __forceinline__ bool x_apart(const XShape& A, const XShape& B) {
 // swap = true, normal box -> capsule), box-box, or MPR for every pair with a hull. Returns the
 // contact count (<= 4); normals point geom1 -> geom2.
 __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
-                                        f3 (&pos)[BB_MAXPT], float (&dist)[BB_MAXPT], f3 (&nrm)[BB_MAXPT], bool& swap) {
+                                        f3 (&pos)[BB_MAXPT], float (&dist)[BB_MAXPT], f3 (&nrm)[BB_MAXPT], bool& swap,
+                                        int* its = nullptr) {
   swap = false;
   if (A.type == 0 && B.type == PS_GEOM_BOX) {
     swap = true;
@@ -476,7 +500,7 @@ __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XS
   }
   float depth;
   f3 n, p;
-  const int cnt = mpr_penetration(m, A, B, &depth, &n, &p);
+  const int cnt = mpr_penetration(m, A, B, &depth, &n, &p, its);
   if (n.x == 0.f && n.y == 0.f && n.z == 0.f) n = mk3(0.f, 0.f, 1.f);
   pos[0] = p;
   nrm[0] = n;

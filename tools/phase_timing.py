@@ -13,7 +13,7 @@ L = lib.load()
 L.ps_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
 NAME = sys.argv[2] if len(sys.argv) > 2 else "crossing_field"
 g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle", **(
-    {"hand_xml": dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand())} if __import__("os").environ.get("PIANOSIM_HULL") else {})), device="cuda:0")
+    {"primitive_fingertip_collisions": False} if __import__("os").environ.get("PIANOSIM_HULL") else {})), device="cuda:0")
 g.reset()
 L.ps_debug_timing(g._h, None)
 gen = torch.Generator(device="cuda:0").manual_seed(1)
@@ -22,12 +22,14 @@ for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
     stats.append(g.solver_stats().cpu().numpy())
 st = np.stack(stats)  # [10, N, 4]
-out = np.zeros((N, 28), np.uint64)
+NPH = 40
+out = np.zeros((N, NPH), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
 names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest",
          11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs", 18: "newton:prep", 3: "factor", 4: "solve_smooth",
          12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
-         8: "nt:J'f", 6: "integrate", 5: "final+task"}
+         8: "nt:J'f", 6: "integrate", 5: "final+task", 32: "xpiano:cand", 33: "xpiano:refine", 34: "xpiano:narrow",
+         35: "xpairs:sphere", 36: "xpairs:refine", 37: "xpairs:narrow"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)
 for i, n in names.items():
     v = out[:, i].astype(np.float64)
@@ -40,6 +42,10 @@ print(f"Newton: iterations per substep mean {solves.mean():.3f}, max over env-st
 # iterations by substep (timing-build counters 19-23): the first substep starts cold, the later
 # ones from the previous substep's zones (one iteration when that piece holds)
 c = out[:, 19:24].astype(np.float64).sum(axis=0)
+m = out[:, 28:32].astype(np.float64).sum(axis=0)  # box / hull narrow-phase rounds (timing build)
+if m[1] > 0 or m[3] > 0:
+    print(f"box/hull narrow phase: piano {m[1] / N / 100:.2f} rounds/substep, {m[0] / max(m[1], 1):.1f} MPR steps of the "
+          f"slowest lane per round; hand-hand {m[3] / N / 100:.2f} rounds/substep, {m[2] / max(m[3], 1):.1f} steps")
 if c[1] > 0 and c[4] > 0:
     print(f"Newton by substep: first {c[0] / c[1]:.2f} iterations, later {c[2] / c[4]:.2f} "
           f"(guessed piece held in {100 * c[3] / c[4]:.1f}% of the later substeps)")

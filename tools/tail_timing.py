@@ -16,7 +16,7 @@ STEPS = 20
 L = lib.load()
 L.ps_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
 g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle", **(
-    {"hand_xml": dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand())} if __import__("os").environ.get("PIANOSIM_HULL") else {})), device="cuda:0")
+    {"primitive_fingertip_collisions": False} if __import__("os").environ.get("PIANOSIM_HULL") else {})), device="cuda:0")
 g.reset()
 gen = torch.Generator(device="cuda:0").manual_seed(1)
 for _ in range(3):
@@ -27,7 +27,7 @@ names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB level
          12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
          8: "nt:J'f", 6: "integrate", 5: "final+task"}  # the slots of phase_timing.py (Newton solve)
 idx = list(names)
-out = np.zeros((N, 28), np.uint64)
+out = np.zeros((N, 40), np.uint64)
 means, maxes, worst_rows, mean_rows, ms, piv = [], [], [], [], [], []
 for s in range(STEPS):
     a = torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1

@@ -20,7 +20,7 @@ def throughput(name, n, steps=20):
     task = dp.TaskConfig(trim_silence=name != "twinkle",
                          solver_iterations=None if its is None else int(its))
     if os.environ.get("PIANOSIM_HULL"):  # the box / hull-fingertip hand (reference default colliders)
-        task = dp.TaskConfig(trim_silence=name != "twinkle", hand_xml=dp.mjcf.hand_to_mjcf(dp.mjcf.box_hull_hand()))
+        task = dp.TaskConfig(trim_silence=name != "twinkle", primitive_fingertip_collisions=False)
     g = dp.BatchedPianoEnv(n, song(dp, name), task, device="cuda:0")
     g.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(12345)

@@ -23,6 +23,7 @@ __device__ XShape unpack(const float* p) {
   s.hs = ld3(p + 20);
   s.v0 = (int)p[23];
   s.nv = (int)p[24];
+  s.hx = s.hz = nullptr;
   if (s.type == 0) s.c = (s.p0 + s.p1) * 0.5f;
   return s;
 }
