@@ -23,7 +23,7 @@ EXPORTS = (
 # Every entry point declared in include/pianorl.h.
 RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample",
               "prl_clip_adam", "prl_gather_minibatch", "prl_lnrelu_fwd", "prl_lnrelu_bwd", "prl_actor_head",
-              "prl_critic_head", "prl_colsums", "prl_mlp_step_work", "prl_mlp_step")
+              "prl_critic_head", "prl_colsums", "prl_mlp_step_work", "prl_mlp_step", "prl_mlp_step_idx")
 
 
 class PrlLayer(C.Structure):  # prl_layer of include/pianorl.h
@@ -118,6 +118,8 @@ def load_rl() -> C.CDLL:
         L.prl_mlp_step_work.argtypes = [C.POINTER(PrlNet), i32, i32]
         L.prl_mlp_step.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, i32, f32, f32, f32, u64, vp, vp, vp,
                                    C.c_size_t, vp]
+        L.prl_mlp_step_idx.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, vp, i32, f32, f32, f32, u64, vp,
+                                       vp, vp, C.c_size_t, vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
     if hasattr(L, "prl_mlp_step_work"):

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <string>
@@ -240,6 +241,7 @@ __global__ void __launch_bounds__(ADAM_THREADS) grad_sumsq_kernel(const float* _
   __shared__ double red[ADAM_THREADS / 64];
   for (int s = 0; s < sg.n; s++) {
     double acc = 0.0;
+#pragma unroll 8
     for (int64_t i = seg_begin(sg, s) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.end[s];
          i += (int64_t)gridDim.x * blockDim.x) {
       const double x = (double)g[i];
@@ -254,6 +256,7 @@ __global__ void __launch_bounds__(ADAM_THREADS) grad_sumsq_kernel(const float* _
 // pass 2: every block folds the partials into the clip coefficient of each segment
 // (torch.nn.utils.clip_grad_norm_: coef = min(1, max_norm / (||g|| + 1e-6))), then the Adam
 // update (torch.optim.Adam, amsgrad/weight_decay off) over a grid-stride range
+constexpr int ADAM_PER = 4;  // elements per thread and pass (their loads issued before the norm fold)
 __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                                  float* __restrict__ m, float* __restrict__ v, Segs sg,
                                                                  const double* __restrict__ part,
@@ -262,6 +265,20 @@ __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restri
                                                                  float eps, float max_norm, int nparts) {
   __shared__ double red[ADAM_THREADS / 64];
   __shared__ float coef[PRL_MAX_SEG], ssz[PRL_MAX_SEG], ibc2[PRL_MAX_SEG];
+  const int64_t n = sg.end[sg.n - 1];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the first pass's operands in flight while the block folds the norm partials
+  float gq[ADAM_PER], mq[ADAM_PER], vq[ADAM_PER], pq[ADAM_PER];
+#pragma unroll
+  for (int u = 0; u < ADAM_PER; u++) {
+    const int64_t i = i0 + u * stride;
+    const bool ok = i < n;
+    gq[u] = ok ? g[i] : 0.f;
+    mq[u] = ok ? m[i] : 0.f;
+    vq[u] = ok ? v[i] : 0.f;
+    pq[u] = ok ? p[i] : 0.f;
+  }
   for (int s = 0; s < sg.n; s++) {
     double acc = 0.0;
     for (int b = threadIdx.x; b < nparts; b += blockDim.x) acc += part[b * PRL_MAX_SEG + s];
@@ -276,18 +293,21 @@ __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restri
     }
   }
   __syncthreads();
-  const int64_t n = sg.end[sg.n - 1];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  auto upd = [&](int64_t i, float gv, float mv, float vv, float pv) {
     int s = 0;
 #pragma unroll
     for (int k = 0; k < PRL_MAX_SEG - 1; k++) s += (k + 1 < sg.n && i >= sg.end[k]) ? 1 : 0;
-    const float gi = g[i] * coef[s];
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    const float gi = gv * coef[s];
+    const float mi = mv + (1.f - b1) * (gi - mv);  // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = b2 * vv + (1.f - b2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    p[i] -= ssz[s] * mi / (sqrtf(vi) * ibc2[s] + eps);
-  }
+    p[i] = pv - ssz[s] * mi / (sqrtf(vi) * ibc2[s] + eps);
+  };
+#pragma unroll
+  for (int u = 0; u < ADAM_PER; u++)
+    if (i0 + u * stride < n) upd(i0 + u * stride, gq[u], mq[u], vq[u], pq[u]);
+  for (int64_t i = i0 + ADAM_PER * stride; i < n; i += stride) upd(i, g[i], m[i], v[i], p[i]);
 }
 
 
@@ -554,7 +574,7 @@ int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_av
   const int parts = (int)std::min<int64_t>(ADAM_PARTS, (n + ADAM_THREADS - 1) / ADAM_THREADS);
   grad_sumsq_kernel<<<parts, ADAM_THREADS, 0, (hipStream_t)stream>>>(grad, sg, scratch, step);
   HIPCHK(hipGetLastError());
-  const int blocks = (int)std::min<int64_t>(1024, (n + ADAM_THREADS * 4 - 1) / (ADAM_THREADS * 4));
+  const int blocks = (int)std::min<int64_t>(2048, (n + ADAM_THREADS * ADAM_PER - 1) / (ADAM_THREADS * ADAM_PER));
   clip_adam_kernel<<<blocks, ADAM_THREADS, 0, (hipStream_t)stream>>>(param, grad, exp_avg, exp_avg_sq, sg, scratch, lr,
                                                                     step, beta1, beta2, eps, max_norm, parts);
   HIPCHK(hipGetLastError());
@@ -716,7 +736,10 @@ int mlp_layout(const prl_net* nets, int sdim, int B, float* work, float* log_row
   a->total = off;
   const int ntiles = (B + mlp::MT - 1) / mlp::MT;
   const size_t npart = (size_t)ntiles * off;
+  const size_t sg_off = scratch;  // then the gathered state rows [B][sdim] (prl_mlp_step_idx)
+  scratch += (size_t)B * sdim;
   *work_floats = npart + scratch;
+  a->Sg = work ? work + npart + sg_off : nullptr;
   if (!work) return 0;  // size query
   // pointers: partial rows, then the scratch
   g->ne = ne;
@@ -758,9 +781,16 @@ size_t prl_mlp_step_work(const prl_net* nets, int sdim, int B) {
   return wf;
 }
 
-int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
-                 const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
-                 const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream) {
+}  // extern "C"
+
+namespace {
+// prl_mlp_step / prl_mlp_step_idx: idx = nullptr takes rows 0..B-1 of S / A / ...; otherwise the
+// rows idx[0..B), read in place by the rows kernel, with the dropout step counter advanced once
+// (by the gradient kernel, after the rows kernel read it)
+int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
+             const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef, float ln_eps,
+             uint64_t seed, uint64_t* step_inc, const uint64_t* step, float* log_row, float* work, size_t work_floats,
+             void* stream) {
   if (!nets || !S || !A || !old_lp || !adv || !ret || !step || !log_row || !work) return fail("prl_mlp_step: null argument");
   if (B <= 0 || sdim <= 0 || sdim > 1024) return fail("prl_mlp_step: B > 0 and 0 < sdim <= 1024 required");
   mlp::Args a{};
@@ -769,15 +799,15 @@ int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, 
   if (mlp_layout(nets, sdim, B, work, log_row, &a, &g, &need)) return -1;
   if (nets[0].layer[3].out != adim) return fail("prl_mlp_step: actor output width != action dim");
   if (work_floats < need) return fail("prl_mlp_step: work space too small (prl_mlp_step_work)");
-  const int KS = ((sdim + 15) & ~15) + 4;
-  const size_t lds = mlp::lds_floats(KS) * sizeof(float);
-  if (lds > 160 * 1024) return fail("prl_mlp_step: state too wide for the LDS tile");
+  const size_t lds = mlp::lds_floats(((sdim + 15) & ~15) + 4) * sizeof(float);
+  if (lds > 150 * 1024) return fail("prl_mlp_step: state too wide for the LDS tile");
   a.nnets = 2;
   a.S = S;
   a.A = A;
   a.LP = old_lp;
   a.ADV = adv;
   a.RET = ret;
+  a.idx = nullptr;
   a.sdim = sdim;
   a.adim = adim;
   a.B = B;
@@ -789,10 +819,17 @@ int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, 
   a.part = work;
   g.X[0] = S;
   g.X[mlp::MAXL] = S;
+  g.step_inc = nullptr;
+  if (idx) {  // gathered in the rows kernel; the weight gradient reads its copy Sg
+    a.idx = idx;
+    g.X[0] = g.X[mlp::MAXL] = a.Sg;
+    g.step_inc = step_inc;
+  }
+  a.Sg = a.idx ? a.Sg : nullptr;
   static bool attr_set = false;
   if (!attr_set) {
     HIPCHK(hipFuncSetAttribute((const void*)mlp::mlp_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024));
+                               150 * 1024));  // (+ its static LDS)
     attr_set = true;
   }
   hipLaunchKernelGGL(mlp::mlp_rows_kernel, dim3(g.ntiles, 2), dim3(mlp::NT), lds, (hipStream_t)stream, a);
@@ -802,6 +839,24 @@ int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, 
                      (hipStream_t)stream, g);
   HIPCHK(hipGetLastError());
   return 0;
+}
+}  // namespace
+
+extern "C" {
+int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
+                 const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
+                 const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream) {
+  return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, nullptr, B, clip, ent_coef, ln_eps, seed, nullptr, step,
+                  log_row, work, work_floats, stream);
+}
+
+int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
+                     const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef,
+                     float ln_eps, uint64_t seed, uint64_t* step, float* log_row, float* work, size_t work_floats,
+                     void* stream) {
+  if (!idx) return fail("prl_mlp_step_idx: null idx");
+  return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, idx, B, clip, ent_coef, ln_eps, seed, step, step, log_row,
+                  work, work_floats, stream);
 }
 
 #ifdef MLP_TIMING

@@ -337,6 +337,9 @@ class FusedStep:
     def __init__(self, agent: "PPOAgent"):
         self.agent = agent
         self.mfma = os.environ.get("PIANORL_NO_MFMA") is None
+        # the rows kernel gathers the minibatch itself (prl_mlp_step_idx); PIANORL_GATHER=1 keeps
+        # the separate gather launch (A/B)
+        self.fused_gather = os.environ.get("PIANORL_GATHER") is None
         self.nets = {}
         a, c = agent.actor.network, agent.critic.network
         # (linear, layernorm, dropout p) per hidden layer, then the output linear
@@ -431,6 +434,17 @@ class FusedStep:
         sdim, adim = ag._S.shape[1], ag._A.shape[1]
         chk = _lib.check_rl
         train = ag.critic.training
+        if self._mlp_ok(B) and self.fused_gather:  # the rows kernel reads the minibatch rows in place
+            nets = self._mlp_nets(train)
+            if "_mlp_work" not in b:
+                n = R.prl_mlp_step_work(nets, sdim, B)
+                b["_mlp_work"] = torch.empty(max(int(n), 1), device=ag.device, dtype=torch.float32)
+            w = b["_mlp_work"]
+            chk(R.prl_mlp_step_idx(nets, ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(),
+                                   ag._ADV.data_ptr(), ag._RET.data_ptr(), idx.data_ptr(), B, float(ag.epsilon),
+                                   float(ag.entropy_coef), float(self.actor[0][0][1].eps), self.seed,
+                                   self.step.data_ptr(), ag._log_row.data_ptr(), w.data_ptr(), w.numel(), st))
+            return
         chk(R.prl_gather_minibatch(ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(), ag._ADV.data_ptr(),
                                    ag._RET.data_ptr(), idx.data_ptr(), B, b["S"].data_ptr(), b["A"].data_ptr(),
                                    b["LP"].data_ptr(), b["ADV"].data_ptr(), b["RET"].data_ptr(), self.step.data_ptr(), st))

@@ -140,6 +140,13 @@ size_t prl_mlp_step_work(const prl_net* nets, int sdim, int B);
 int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
                  const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
                  const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream);
+/* prl_gather_minibatch + prl_mlp_step in one: S / A / old_lp / adv / ret are the whole rollout
+ * ([N, sdim] ...), the minibatch is rows idx[B] (int64), read in place by the rows kernel; the
+ * dropout step counter *step is advanced once (as prl_gather_minibatch does). Same work size. */
+int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
+                     const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef,
+                     float ln_eps, uint64_t seed, uint64_t* step, float* log_row, float* work, size_t work_floats,
+                     void* stream);
 
 #ifdef __cplusplus
 }

@@ -33,6 +33,13 @@ fi
 timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 > profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/throughput.py twinkle 1024 4096 >> profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/ppo_bench.py --mode reference --iters 3 --warmup 2 > profiles/${P}_ppo_bench.jsonl 2>/dev/null || exit 8
+# the PPO loop's kernels (TunableOp off: no GEMM tuning launches in the trace)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${P}_ppo_trace -- python tools/ppo_bench.py --mode reference --iters 2 --warmup 1 --no-tune > gpurun_out/${P}_ppo_trace.log 2>&1 || exit 8
+find gpurun_out/${P}_ppo_trace -name "*kernel_stats.csv" -exec cp {} profiles/${P}_ppo_kernel_stats.csv \;
+# the coupled-block LDL' on the matrix cores against the register method (tools/ldl_bench.hip)
+if [ -f tools/libldlbench.so ]; then
+  timeout -k 10 120 python tools/ldl_bench.py > profiles/${P}_ldl_bench.jsonl 2>/dev/null || exit 8
+fi
 # the reference's default collider kinds (palm boxes, hull fingertips): pianosim_kernel<true>
 if [ -z "$SKIP_HULL" ]; then
   H=${P}_hull
