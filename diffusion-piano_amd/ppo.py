@@ -392,9 +392,11 @@ class FusedStep:
         self.bufs[B] = b
         return b
 
-    def __call__(self, idx):
+    def __call__(self, idx, log_row=None):
+        """One minibatch step; the logged means go to ``log_row`` where the matrix-core step
+        runs (returns True), else to the agent's ``_log_row``."""
         with torch.no_grad():  # the backward is written out: no autograd graph
-            self._step(idx)
+            return self._step(idx, log_row)
 
     def _mlp_nets(self, train):
         """prl_net descriptors of (actor, critic) for prl_mlp_step (cached per dropout mode)."""
@@ -427,7 +429,7 @@ class FusedStep:
                         for lin, _, _ in self.actor[0] + self.critic[0])
         return hidden_ok and self.actor[1].out_features <= 64 and self.agent._S.shape[1] <= 384
 
-    def _step(self, idx):
+    def _step(self, idx, log_row=None):
         ag, R, st = self.agent, _lib.load_rl(), _stream()
         B = idx.numel()
         b = self._buffers(B)
@@ -443,8 +445,9 @@ class FusedStep:
             chk(R.prl_mlp_step_idx(nets, ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(),
                                    ag._ADV.data_ptr(), ag._RET.data_ptr(), idx.data_ptr(), B, float(ag.epsilon),
                                    float(ag.entropy_coef), float(self.actor[0][0][1].eps), self.seed,
-                                   self.step.data_ptr(), ag._log_row.data_ptr(), w.data_ptr(), w.numel(), st))
-            return
+                                   self.step.data_ptr(), (ag._log_row if log_row is None else log_row).data_ptr(),
+                                   w.data_ptr(), w.numel(), st))
+            return log_row is not None
         chk(R.prl_gather_minibatch(ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(), ag._ADV.data_ptr(),
                                    ag._RET.data_ptr(), idx.data_ptr(), B, b["S"].data_ptr(), b["A"].data_ptr(),
                                    b["LP"].data_ptr(), b["ADV"].data_ptr(), b["RET"].data_ptr(), self.step.data_ptr(), st))
@@ -456,9 +459,10 @@ class FusedStep:
             w = b["_mlp_work"]
             chk(R.prl_mlp_step(nets, b["S"].data_ptr(), sdim, b["A"].data_ptr(), adim, b["LP"].data_ptr(),
                                b["ADV"].data_ptr(), b["RET"].data_ptr(), B, float(ag.epsilon), float(ag.entropy_coef),
-                               float(self.actor[0][0][1].eps), self.seed, self.step.data_ptr(), ag._log_row.data_ptr(),
+                               float(self.actor[0][0][1].eps), self.seed, self.step.data_ptr(),
+                               (ag._log_row if log_row is None else log_row).data_ptr(),
                                w.data_ptr(), w.numel(), st))
-            return
+            return log_row is not None
         for net, (hidden, out) in (("a", self.actor), ("c", self.critic)):
             x = b["S"]
             for i, (lin, ln, p) in enumerate(hidden):  # forward
@@ -591,8 +595,9 @@ class PPOAgent:
         if self.fused:
             if self._fused is None:
                 self._fused = FusedStep(self)
-            self._fused(idx)  # writes self._log_row
-            if log_row.data_ptr() != self._log_row.data_ptr():
+            # the matrix-core step writes the log row in place (no copy node per minibatch in
+            # the chunk graph); the per-layer path writes self._log_row
+            if not self._fused(idx, log_row) and log_row.data_ptr() != self._log_row.data_ptr():
                 log_row.copy_(self._log_row)
             return
         b_s = self._S.index_select(0, idx)
