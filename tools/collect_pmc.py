@@ -25,10 +25,15 @@ def rows(d, pattern):
     return out
 
 
+# the profiled instantiation: pianosim_kernel<false> (capsule hand) or <true> (box / hull
+# colliders); bench.py's line also times the other one (its hull leg), which must not mix in
+KNAME = "pianosim_kernel<true>" if __import__("os").environ.get("PIANOSIM_HULL") else "pianosim_kernel<false>"
+
+
 def counter(d, name):
     per_dispatch = defaultdict(float)
     for r in rows(d, "*counter_collection.csv"):
-        if "pianosim_kernel" not in r.get("Kernel_Name", ""):
+        if KNAME not in r.get("Kernel_Name", ""):
             continue
         if r.get("Counter_Name") != name:
             continue
@@ -45,21 +50,21 @@ def main():
     tdir, fdir, wdir, envs, song, prefix = sys.argv[1:4] + [int(sys.argv[4])] + sys.argv[5:7]
     warmup = int(sys.argv[7]) if len(sys.argv) > 7 else 5
     sqdir = sys.argv[8] if len(sys.argv) > 8 else None
-    stats = [r for r in rows(tdir, "*kernel_stats.csv") if "pianosim_kernel" in r.get("Name", "")]
+    stats = [r for r in rows(tdir, "*kernel_stats.csv") if KNAME in r.get("Name", "")]
     fetch_kb = counter(fdir, "FETCH_SIZE")
     write_kb = counter(wdir, "WRITE_SIZE")
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     from bench import lib_sha  # the profiled binary (bench.py quotes only profiles of its own build)
     import os
     hand = "hull" if os.environ.get("PIANOSIM_HULL") else "authored"  # bench.py --hand
-    out = {"envs": envs, "song": song, "hand": hand, "kernel": "pianosim_kernel", "lib_sha": lib_sha()}
+    out = {"envs": envs, "song": song, "hand": hand, "kernel": KNAME, "lib_sha": lib_sha()}
     if stats:
         s = stats[0]
         out["rocprof_avg_ns_all_launches"] = float(s.get("AverageNs", 0))
         out["rocprof_calls"] = int(s.get("Calls", 0))
     # the timed steps only: bench.py launches reset (1) + warmup (5) before the timed region
     tr = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows(tdir, "*kernel_trace.csv")
-                if "pianosim_kernel" in r.get("Kernel_Name", ""))
+                if KNAME in r.get("Kernel_Name", ""))
     timed = [e - b for b, e in tr[1 + warmup:]]
     if timed:
         out["rocprof_avg_ns"] = sum(timed) / len(timed)

@@ -1,7 +1,9 @@
 # One GPU session: parity tests (+ drift report), bench, rocprofv3 kernel trace and the two
 # PMC passes (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE in separate passes).
 # usage (on the box, via gpurun): bash tools/gpu_round.sh <prefix, e.g. r03_v1>
-# (SKIP_HULL=1: without the box/hull-hand bench, profiles and throughput)
+# (SKIP_HULL=1: without the box/hull-hand bench, profiles and throughput; PART=1: the tests, bench
+# and capsule-hand profiles only; PART=2: throughput, PPO, LDL' and hull parts only - two calls
+# when one would not fit gpurun's time limit)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -9,16 +11,17 @@ P=${1:-r01}
 SONG=crossing_field
 mkdir -p gpurun_out profiles
 rm -rf gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write gpurun_out/${P}_sq
+if [ "${PART:-all}" != 2 ]; then
 PIANOSIM_REPORT=profiles/${P}_drift.json timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 RC=$?
 echo "PYTEST_EXIT $RC" >> gpurun_out/pytest_gpu.log
 # 0 = green, 1 = a failed assertion; anything else (fault, abort, time limit) ends the call
 if [ $RC -gt 1 ]; then exit 9; fi
 cp profiles/${P}_drift.json profiles/drift_latest.json 2>/dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${P}_trace -- python bench.py --no-cpu-baseline --steps 20 > gpurun_out/${P}_trace.log 2>&1 || exit 2
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${P}_fetch -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/${P}_fetch.log 2>&1 || exit 3
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${P}_write -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/${P}_write.log 2>&1 || exit 4
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d gpurun_out/${P}_sq -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/${P}_sq.log 2>&1 || exit 7
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${P}_trace -- python bench.py --no-cpu-baseline --no-hull-leg --steps 20 > gpurun_out/${P}_trace.log 2>&1 || exit 2
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${P}_fetch -- python bench.py --no-cpu-baseline --no-hull-leg --steps 10 > gpurun_out/${P}_fetch.log 2>&1 || exit 3
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${P}_write -- python bench.py --no-cpu-baseline --no-hull-leg --steps 10 > gpurun_out/${P}_write.log 2>&1 || exit 4
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d gpurun_out/${P}_sq -- python bench.py --no-cpu-baseline --no-hull-leg --steps 10 > gpurun_out/${P}_sq.log 2>&1 || exit 7
 python tools/collect_pmc.py gpurun_out/${P}_trace gpurun_out/${P}_fetch gpurun_out/${P}_write 4096 $SONG $P 5 gpurun_out/${P}_sq > gpurun_out/pmc.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
 cp gpurun_out/bench.json profiles/${P}_bench.json
@@ -30,6 +33,8 @@ fi
 if [ -f diffusion-piano_amd/libpianosim_timing.so ]; then
   PIANOSIM_LIB=diffusion-piano_amd/libpianosim_timing.so timeout -k 10 120 python tools/tail_timing.py 1024 twinkle > profiles/${P}_tail_1024.txt 2>/dev/null || exit 5
 fi
+fi
+if [ "${PART:-all}" != 1 ]; then
 timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 > profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/throughput.py twinkle 1024 4096 >> profiles/${P}_throughput.txt 2>/dev/null || exit 6
 timeout -k 10 200 python tools/ppo_bench.py --mode reference --iters 3 --warmup 2 > profiles/${P}_ppo_bench.jsonl 2>/dev/null || exit 8
@@ -55,6 +60,7 @@ if [ -z "$SKIP_HULL" ]; then
   fi
   timeout -k 10 200 python tools/throughput.py crossing_field 1024 4096 16384 > profiles/${H}_throughput.txt 2>/dev/null || exit 15
   unset PIANOSIM_HULL
+fi
 fi
 cp -r profiles gpurun_out/profiles_new
 echo DONE
