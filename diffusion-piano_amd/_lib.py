@@ -17,13 +17,14 @@ EXPORTS = (
     "ps_reset", "ps_step", "ps_get_state", "ps_set_state", "ps_set_applied", "ps_reward_terms",
     "ps_fingertips", "ps_contact_count", "ps_musical_metrics", "ps_solver_stats", "ps_get_hand_offset",
     "ps_set_hand_offset", "ps_record_contacts", "ps_contacts", "ps_set_env_offset", "ps_warnings",
-    "ps_env_obs_dim", "ps_env_action_dim",
+    "ps_env_obs_dim", "ps_env_action_dim", "ps_episode_returns",
 )
 
 # Every entry point declared in include/pianorl.h.
 RL_EXPORTS = ("prl_last_error", "prl_version", "prl_running_norm", "prl_gae", "prl_normalize", "prl_gauss_sample",
               "prl_clip_adam", "prl_gather_minibatch", "prl_lnrelu_fwd", "prl_lnrelu_bwd", "prl_actor_head",
-              "prl_critic_head", "prl_colsums", "prl_mlp_step_work", "prl_mlp_step", "prl_mlp_step_idx")
+              "prl_critic_head", "prl_colsums", "prl_mlp_step_work", "prl_mlp_step", "prl_mlp_step_idx",
+              "prl_mlp_step_norm_parts", "prl_mlp_step_idx_norm", "prl_clip_adam_parts")
 
 
 class PrlLayer(C.Structure):  # prl_layer of include/pianorl.h
@@ -70,6 +71,8 @@ def load() -> C.CDLL:
     L.ps_musical_metrics.argtypes = [vp, vp, vp, vp]
     if hasattr(L, "ps_record_contacts"):
         L.ps_record_contacts.argtypes = [vp, i32]
+    if hasattr(L, "ps_episode_returns"):
+        L.ps_episode_returns.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
     if hasattr(L, "ps_set_env_offset"):
         L.ps_set_env_offset.argtypes = [vp, C.c_int64]
     for name, argc in (("ps_solver_stats", 3), ("ps_get_hand_offset", 4), ("ps_set_hand_offset", 3),
@@ -120,6 +123,11 @@ def load_rl() -> C.CDLL:
                                    C.c_size_t, vp]
         L.prl_mlp_step_idx.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, vp, i32, f32, f32, f32, u64, vp,
                                        vp, vp, C.c_size_t, vp]
+        L.prl_mlp_step_norm_parts.argtypes = [C.POINTER(PrlNet), i32, i32]
+        L.prl_mlp_step_idx_norm.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, vp, i32, f32, f32, f32, u64,
+                                            vp, vp, vp, C.c_size_t, vp, C.POINTER(C.c_int64), i32, vp, vp, i32, vp]
+        L.prl_clip_adam_parts.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_int64), i32, vp, vp, f32, f32, f32, f32, vp, i32,
+                                          vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
     if hasattr(L, "prl_mlp_step_work"):

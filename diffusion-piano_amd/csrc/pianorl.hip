@@ -557,10 +557,12 @@ int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint
   return 0;
 }
 
-int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
-                  int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
-                  double* scratch, void* stream) {
-  if (!param || !grad || !exp_avg || !exp_avg_sq || !seg_end || !lr || !step || !scratch)
+}  // extern "C"
+namespace {
+int clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end, int nseg,
+              const float* lr, float* step, float beta1, float beta2, float eps, float max_norm, double* scratch,
+              const double* pre_parts, int npre, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !seg_end || !lr || !step || (!scratch && !pre_parts))
     return fail("prl_clip_adam: null pointer");
   if (nseg < 1 || nseg > PRL_MAX_SEG) return fail("prl_clip_adam: need 1 <= nseg <= PRL_MAX_SEG");
   Segs sg{};
@@ -572,6 +574,13 @@ int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_av
   for (int s = nseg; s < PRL_MAX_SEG; s++) sg.end[s] = sg.end[nseg - 1];
   const int64_t n = sg.end[nseg - 1];
   const int parts = (int)std::min<int64_t>(ADAM_PARTS, (n + ADAM_THREADS - 1) / ADAM_THREADS);
+  if (pre_parts) {  // the norm partials (and the step advance) came from prl_mlp_step_norm
+    const int blocks = (int)std::min<int64_t>(2048, (n + ADAM_THREADS * ADAM_PER - 1) / (ADAM_THREADS * ADAM_PER));
+    clip_adam_kernel<<<blocks, ADAM_THREADS, 0, (hipStream_t)stream>>>(param, grad, exp_avg, exp_avg_sq, sg, pre_parts,
+                                                                      lr, step, beta1, beta2, eps, max_norm, npre);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   grad_sumsq_kernel<<<parts, ADAM_THREADS, 0, (hipStream_t)stream>>>(grad, sg, scratch, step);
   HIPCHK(hipGetLastError());
   const int blocks = (int)std::min<int64_t>(2048, (n + ADAM_THREADS * ADAM_PER - 1) / (ADAM_THREADS * ADAM_PER));
@@ -579,6 +588,23 @@ int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_av
                                                                     step, beta1, beta2, eps, max_norm, parts);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+}  // namespace
+extern "C" {
+int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
+                  int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
+                  double* scratch, void* stream) {
+  return clip_adam(param, grad, exp_avg, exp_avg_sq, seg_end, nseg, lr, step, beta1, beta2, eps, max_norm, scratch,
+                   nullptr, 0, stream);
+}
+
+int prl_clip_adam_parts(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
+                        int nseg, const float* lr, const float* step, float beta1, float beta2, float eps,
+                        float max_norm, const double* parts, int nparts, void* stream) {
+  if (!parts || nparts <= 0) return fail("prl_clip_adam_parts: no partials");
+  return clip_adam(param, grad, exp_avg, exp_avg_sq, seg_end, nseg, lr, const_cast<float*>(step), beta1, beta2, eps,
+                   max_norm, nullptr, parts, nparts, stream);
 }
 
 int prl_gather_minibatch(const float* S, int sdim, const float* A, int adim, const float* lp, const float* adv,
@@ -679,7 +705,7 @@ int mlp_layout(const prl_net* nets, int sdim, int B, float* work, float* log_row
   int off = 0, ne = 0;
   auto entry = [&](int n, float* dst, float scale) {
     if (ne >= mlp::MAXRED) return -1;
-    g->e[ne] = mlp::RedEntry{off, n, scale, dst};
+    g->e[ne] = mlp::RedEntry{off, n, scale, dst, -1};
     ne++;
     const int o = off;
     off += n;
@@ -740,14 +766,21 @@ int mlp_layout(const prl_net* nets, int sdim, int B, float* work, float* log_row
   scratch += (size_t)B * sdim;
   *work_floats = npart + scratch;
   a->Sg = work ? work + npart + sg_off : nullptr;
-  if (!work) return 0;  // size query
-  // pointers: partial rows, then the scratch
   g->ne = ne;
+  g->rfirst[0] = 0;
+  for (int e = 0; e < ne; e++) g->rfirst[e + 1] = g->rfirst[e] + (g->e[e].n + 63) / 64;
+  int qtiles = 0;
+  for (int i = 0; i < 2; i++)
+    for (int l = 0; l < mlp::MAXL; l++) {
+      const mlp::Layer& o = a->net[i].L[l];
+      qtiles += ((o.out + 15) / 16) * ((o.in + 15) / 16);
+    }
+  g->ntw = qtiles;
+  if (!work) return 0;  // size query (ne, rfirst, ntw: the gradient kernel's wave count)
+  // pointers: partial rows, then the scratch
   g->total = off;
   g->ntiles = ntiles;
   g->part = work;
-  g->rfirst[0] = 0;
-  for (int e = 0; e < ne; e++) g->rfirst[e + 1] = g->rfirst[e] + (g->e[e].n + 63) / 64;
   int gl = 0, tiles = 0;
   for (int i = 0; i < 2; i++)
     for (int l = 0; l < mlp::MAXL; l++) {
@@ -781,16 +814,33 @@ size_t prl_mlp_step_work(const prl_net* nets, int sdim, int B) {
   return wf;
 }
 
+int prl_mlp_step_norm_parts(const prl_net* nets, int sdim, int B) {
+  mlp::Args a{};
+  mlp::GradArgs g{};
+  float dummy;
+  size_t wf = 0;
+  if (!nets || B <= 0 || sdim <= 0 || mlp_layout(nets, sdim, B, nullptr, &dummy, &a, &g, &wf)) return 0;
+  return ((g.ntw + g.rfirst[g.ne] + mlp::GWV - 1) / mlp::GWV) * mlp::GWV;
+}
+
 }  // extern "C"
 
 namespace {
 // prl_mlp_step / prl_mlp_step_idx: idx = nullptr takes rows 0..B-1 of S / A / ...; otherwise the
 // rows idx[0..B), read in place by the rows kernel, with the dropout step counter advanced once
 // (by the gradient kernel, after the rows kernel read it)
+struct NormOut {  // prl_mlp_step_idx_norm: the grad-norm partials for prl_clip_adam_parts
+  const float* grad_base;
+  const int64_t* seg_end;
+  int nseg;
+  float* adam_step;
+  double* part;
+  int nparts;
+};
 int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
              const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef, float ln_eps,
              uint64_t seed, uint64_t* step_inc, const uint64_t* step, float* log_row, float* work, size_t work_floats,
-             void* stream) {
+             void* stream, const NormOut* no = nullptr) {
   if (!nets || !S || !A || !old_lp || !adv || !ret || !step || !log_row || !work) return fail("prl_mlp_step: null argument");
   if (B <= 0 || sdim <= 0 || sdim > 1024) return fail("prl_mlp_step: B > 0 and 0 < sdim <= 1024 required");
   mlp::Args a{};
@@ -826,6 +876,30 @@ int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int 
     g.step_inc = step_inc;
   }
   a.Sg = a.idx ? a.Sg : nullptr;
+  g.npart = nullptr;
+  if (no) {  // each gradient write's clip+Adam segment, from its offset in the flat gradient buffer
+    if (!no->grad_base || !no->seg_end || no->nseg < 1 || no->nseg > PRL_MAX_SEG || !no->adam_step || !no->part)
+      return fail("prl_mlp_step_idx_norm: bad optimiser arguments");
+    auto seg_of = [&](const float* p) {
+      const int64_t o = p - no->grad_base;
+      for (int s = 0; s < no->nseg; s++)
+        if (o >= 0 && o < no->seg_end[s]) return s;
+      return -1;
+    };
+    for (int l = 0; l < g.nl; l++) {
+      g.seg[l] = seg_of(g.dW[l]);
+      if (g.seg[l] < 0) return fail("prl_mlp_step_idx_norm: a weight gradient outside the segments");
+    }
+    for (int e = 0; e < g.ne; e++) {
+      g.e[e].seg = g.e[e].dst == log_row ? -1 : seg_of(g.e[e].dst);
+      if (g.e[e].dst != log_row && g.e[e].seg < 0) return fail("prl_mlp_step_idx_norm: a gradient outside the segments");
+    }
+    const int waves = ((g.ntw + g.rfirst[g.ne] + mlp::GWV - 1) / mlp::GWV) * mlp::GWV;
+    if (no->nparts < waves) return fail("prl_mlp_step_idx_norm: partial buffer too small (prl_mlp_step_norm_parts)");
+    g.npart = no->part;
+    g.adam_step = no->adam_step;
+    g.nseg = no->nseg;
+  }
   static bool attr_set = false;
   if (!attr_set) {
     HIPCHK(hipFuncSetAttribute((const void*)mlp::mlp_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -857,6 +931,17 @@ int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float*
   if (!idx) return fail("prl_mlp_step_idx: null idx");
   return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, idx, B, clip, ent_coef, ln_eps, seed, step, step, log_row,
                   work, work_floats, stream);
+}
+
+int prl_mlp_step_idx_norm(const prl_net* nets, const float* S, int sdim, const float* A, int adim,
+                          const float* old_lp, const float* adv, const float* ret, const int64_t* idx, int B,
+                          float clip, float ent_coef, float ln_eps, uint64_t seed, uint64_t* step, float* log_row,
+                          float* work, size_t work_floats, const float* grad_base, const int64_t* seg_end, int nseg,
+                          float* adam_step, double* norm_part, int nparts, void* stream) {
+  if (!idx) return fail("prl_mlp_step_idx_norm: null idx");
+  const NormOut no{grad_base, seg_end, nseg, adam_step, norm_part, nparts};
+  return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, idx, B, clip, ent_coef, ln_eps, seed, step, step, log_row,
+                  work, work_floats, stream, &no);
 }
 
 #ifdef MLP_TIMING

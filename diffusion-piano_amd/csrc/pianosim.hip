@@ -872,6 +872,53 @@ int ps_set_env_offset(ps_env* E, int64_t global_first_env) {
   return 0;
 }
 
+// one workgroup: env i by thread i (mod 1024); the finished episodes' sum in a fixed order
+// (per-thread partials, then a tree over the 1024 threads): deterministic
+__global__ void __launch_bounds__(1024) episode_returns_kernel(const float* __restrict__ reward,
+                                                               const uint8_t* __restrict__ step_type, int n,
+                                                               double* __restrict__ running, float* __restrict__ last_return,
+                                                               double* __restrict__ finished_sum,
+                                                               int64_t* __restrict__ finished_count) {
+  __shared__ double ssum[1024];
+  __shared__ int scnt[1024];
+  double fs = 0.0;
+  int fc = 0;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const int st = step_type[i];
+    const double r = st == PS_FIRST ? 0.0 : running[i] + (double)reward[i];
+    running[i] = r;
+    if (st == PS_LAST) {
+      last_return[i] = (float)r;
+      fs += r;
+      fc++;
+    }
+  }
+  ssum[threadIdx.x] = fs;
+  scnt[threadIdx.x] = fc;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      ssum[threadIdx.x] += ssum[threadIdx.x + w];
+      scnt[threadIdx.x] += scnt[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *finished_sum += ssum[0];
+    *finished_count += scnt[0];
+  }
+}
+
+int ps_episode_returns(const float* reward, const uint8_t* step_type, int n, double* running, float* last_return,
+                       double* finished_sum, int64_t* finished_count, void* stream) {
+  if (!reward || !step_type || !running || !last_return || !finished_sum || !finished_count || n <= 0)
+    return fail("ps_episode_returns: null argument or n <= 0");
+  hipLaunchKernelGGL(episode_returns_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, reward, step_type, n, running,
+                     last_return, finished_sum, finished_count);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int ps_contact_count(ps_env* E, int32_t* ncon, void* stream) {
   if (!E || !ncon) return fail("null argument");
   GUARD(E);

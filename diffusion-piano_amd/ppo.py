@@ -310,8 +310,20 @@ class FlatAdam(GradBucket):
             self.step_count[s].fill_(float(st["step"]))
         self._bind_state()
 
+    # (ptr, n): gradient-norm partials a fused minibatch step left for the next step() (and the
+    # step counts it advanced), prl_mlp_step_idx_norm
+    pre_parts = None
+
     def step(self):
         b1, b2 = self.betas
+        if self.pre_parts is not None:
+            ptr, n = self.pre_parts
+            self.pre_parts = None
+            _lib.check_rl(_lib.load_rl().prl_clip_adam_parts(
+                self.param.data_ptr(), self.flat.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                self.seg_end, self.nseg, self.lr.data_ptr(), self.step_count.data_ptr(), float(b1), float(b2),
+                float(self.eps), float(self.max_norm), ptr, n, _stream()))
+            return
         _lib.check_rl(_lib.load_rl().prl_clip_adam(
             self.param.data_ptr(), self.flat.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
             self.seg_end, self.nseg, self.lr.data_ptr(), self.step_count.data_ptr(), float(b1), float(b2),
@@ -340,6 +352,9 @@ class FusedStep:
         # the rows kernel gathers the minibatch itself (prl_mlp_step_idx); PIANORL_GATHER=1 keeps
         # the separate gather launch (A/B)
         self.fused_gather = os.environ.get("PIANORL_GATHER") is None
+        # and the gradient kernel leaves the clip norm's partials for FlatAdam (prl_clip_adam_parts);
+        # PIANORL_SUMSQ=1 keeps the separate norm pass (A/B)
+        self.fused_norm = os.environ.get("PIANORL_SUMSQ") is None
         self.nets = {}
         a, c = agent.actor.network, agent.critic.network
         # (linear, layernorm, dropout p) per hidden layer, then the output linear
@@ -442,11 +457,27 @@ class FusedStep:
                 n = R.prl_mlp_step_work(nets, sdim, B)
                 b["_mlp_work"] = torch.empty(max(int(n), 1), device=ag.device, dtype=torch.float32)
             w = b["_mlp_work"]
+            lr_ptr = (ag._log_row if log_row is None else log_row).data_ptr()
+            fl = getattr(ag, "flat", None)
+            if self.fused_norm and isinstance(fl, FlatAdam) and not ag.distributed:
+                # the gradient kernel also leaves clip_grad_norm_'s partials: FlatAdam.step then
+                # runs one launch (no grad_sumsq pass); single process only (no all-reduce between)
+                if "_norm_part" not in b:
+                    b["_norm_part"] = torch.zeros(max(1, R.prl_mlp_step_norm_parts(nets, sdim, B)), 4,
+                                                  device=ag.device, dtype=torch.float64)
+                npart = b["_norm_part"]
+                chk(R.prl_mlp_step_idx_norm(nets, ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(),
+                                            ag._ADV.data_ptr(), ag._RET.data_ptr(), idx.data_ptr(), B,
+                                            float(ag.epsilon), float(ag.entropy_coef), float(self.actor[0][0][1].eps),
+                                            self.seed, self.step.data_ptr(), lr_ptr, w.data_ptr(), w.numel(),
+                                            fl.flat.data_ptr(), fl.seg_end, fl.nseg, fl.step_count.data_ptr(),
+                                            npart.data_ptr(), npart.shape[0], st))
+                fl.pre_parts = (npart.data_ptr(), npart.shape[0])
+                return log_row is not None
             chk(R.prl_mlp_step_idx(nets, ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(),
                                    ag._ADV.data_ptr(), ag._RET.data_ptr(), idx.data_ptr(), B, float(ag.epsilon),
                                    float(ag.entropy_coef), float(self.actor[0][0][1].eps), self.seed,
-                                   self.step.data_ptr(), (ag._log_row if log_row is None else log_row).data_ptr(),
-                                   w.data_ptr(), w.numel(), st))
+                                   self.step.data_ptr(), lr_ptr, w.data_ptr(), w.numel(), st))
             return log_row is not None
         chk(R.prl_gather_minibatch(ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(), ag._ADV.data_ptr(),
                                    ag._RET.data_ptr(), idx.data_ptr(), B, b["S"].data_ptr(), b["A"].data_ptr(),

@@ -54,6 +54,17 @@ class EpisodeReturns:
         """Call after every step: FIRST steps (reward 0 after auto-reset) start a new
         episode, LAST steps close one."""
         torch = self._torch
+        if self.running.is_cuda:  # one launch (libpianosim ps_episode_returns) instead of ~12
+            from . import _lib
+            L = _lib.load()
+            if hasattr(L, "ps_episode_returns"):
+                st = step_type if step_type.dtype == torch.uint8 else step_type.to(torch.uint8)
+                rew = reward if reward.dtype == torch.float32 else reward.to(torch.float32)
+                _lib.check(L.ps_episode_returns(rew.data_ptr(), st.contiguous().data_ptr(), self.running.numel(),
+                                                self.running.data_ptr(), self.last_return.data_ptr(),
+                                                self.finished_sum.data_ptr(), self.finished_count.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream))
+                return
         first = step_type == 0
         self.running = torch.where(first, torch.zeros_like(self.running), self.running + reward.to(torch.float64))
         last = step_type == 2

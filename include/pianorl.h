@@ -71,6 +71,11 @@ int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint
 int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
                   int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
                   double* scratch, void* stream);
+/* prl_clip_adam with the gradient-norm partials already summed per segment (parts [nparts]
+ * [PRL_MAX_SEG] f64, prl_mlp_step_idx_norm) and the step counts already advanced: one launch. */
+int prl_clip_adam_parts(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
+                        int nseg, const float* lr, const float* step, float beta1, float beta2, float eps,
+                        float max_norm, const double* parts, int nparts, void* stream);
 
 /* ---- fused minibatch step (ppo_v2.py:266-293 with the backward written out; the GEMMs
  * between these are library GEMMs). All row-major fp32 [rows, cols]. */
@@ -147,6 +152,17 @@ int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float*
                      const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef,
                      float ln_eps, uint64_t seed, uint64_t* step, float* log_row, float* work, size_t work_floats,
                      void* stream);
+/* prl_mlp_step_idx that also leaves the clip_grad_norm_ partials for prl_clip_adam_parts (one
+ * launch less per minibatch): grad_base = the flat gradient buffer the layers' gradients live
+ * in, seg_end[nseg] its segments (as prl_clip_adam); the gradient kernel writes each wave's sum
+ * of squares per segment into norm_part [nparts][PRL_MAX_SEG] f64 (nparts >=
+ * prl_mlp_step_norm_parts) and advances adam_step[nseg] (the optimisers' step counts) by one. */
+int prl_mlp_step_norm_parts(const prl_net* nets, int sdim, int B);
+int prl_mlp_step_idx_norm(const prl_net* nets, const float* S, int sdim, const float* A, int adim,
+                          const float* old_lp, const float* adv, const float* ret, const int64_t* idx, int B,
+                          float clip, float ent_coef, float ln_eps, uint64_t seed, uint64_t* step, float* log_row,
+                          float* work, size_t work_floats, const float* grad_base, const int64_t* seg_end, int nseg,
+                          float* adam_step, double* norm_part, int nparts, void* stream);
 
 #ifdef __cplusplus
 }

@@ -344,6 +344,14 @@ int ps_solver_stats(ps_env* env, int32_t* stats, void* stream);
  * warning into PhysicsError (Physics.check_invalid_state); envs.Environment does the same. */
 int ps_warnings(ps_env* env, int32_t* warnings, void* stream);
 
+/* Episode-return bookkeeping of a rollout loop in one launch (the reference driver's per-env
+ * return sums, parallelized_base_v2.py / ppo_v2.py training loops): after a step with rewards
+ * reward[n] and step types step_type[n] (uint8), running[i] (f64) restarts at a FIRST step and
+ * accumulates the reward otherwise; at a LAST step last_return[i] (f32) takes it and it is added
+ * to *finished_sum (f64) and *finished_count (int64). Device pointers; no env handle. */
+int ps_episode_returns(const float* reward, const uint8_t* step_type, int n, double* running, float* last_return,
+                       double* finished_sum, int64_t* finished_count, void* stream);
+
 /* randomize_hand_positions (piano_with_shadow_hands.py:491-499): each env's current y shift of
  * both hand roots [N] f32 and its resets so far [N] i32 (device; either may be NULL). The set
  * form overrides the shift until the env's next reset (teacher-forced parity). */
