@@ -62,5 +62,5 @@ if [ -z "$SKIP_HULL" ]; then
   unset PIANOSIM_HULL
 fi
 fi
-cp -r profiles gpurun_out/profiles_new
+rm -rf gpurun_out/profiles_new && cp -r profiles gpurun_out/profiles_new
 echo DONE
