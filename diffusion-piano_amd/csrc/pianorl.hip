@@ -256,14 +256,16 @@ __global__ void __launch_bounds__(ADAM_THREADS) grad_sumsq_kernel(const float* _
 // pass 2: every block folds the partials into the clip coefficient of each segment
 // (torch.nn.utils.clip_grad_norm_: coef = min(1, max_norm / (||g|| + 1e-6))), then the Adam
 // update (torch.optim.Adam, amsgrad/weight_decay off) over a grid-stride range
-constexpr int ADAM_PER = 4;  // elements per thread and pass (their loads issued before the norm fold)
+#ifndef ADAM_PER_N
+#define ADAM_PER_N 4
+#endif
+constexpr int ADAM_PER = ADAM_PER_N;  // elements per thread and pass (their loads issued before the norm fold)
 __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                                  float* __restrict__ m, float* __restrict__ v, Segs sg,
                                                                  const double* __restrict__ part,
                                                                  const float* __restrict__ lr,
                                                                  const float* __restrict__ step, float b1, float b2,
                                                                  float eps, float max_norm, int nparts) {
-  __shared__ double red[ADAM_THREADS / 64];
   __shared__ float coef[PRL_MAX_SEG], ssz[PRL_MAX_SEG], ibc2[PRL_MAX_SEG];
   const int64_t n = sg.end[sg.n - 1];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -279,18 +281,36 @@ __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restri
     vq[u] = ok ? v[i] : 0.f;
     pq[u] = ok ? p[i] : 0.f;
   }
-  for (int s = 0; s < sg.n; s++) {
-    double acc = 0.0;
-    for (int b = threadIdx.x; b < nparts; b += blockDim.x) acc += part[b * PRL_MAX_SEG + s];
-    const double tot = block_sum_d(acc, red);
-    if (threadIdx.x == 0) {
-      const float norm = (float)sqrt(tot);
-      coef[s] = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
-      const double t = (double)step[s];
-      const double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
-      ssz[s] = (float)((double)lr[s] / bc1);
-      ibc2[s] = (float)(1.0 / sqrt(bc2));
+  // every segment's partials in one pass over the rows (each row's PRL_MAX_SEG doubles are one
+  // 32-byte read), then one block reduction of the PRL_MAX_SEG sums - per segment the same
+  // association order as a per-segment fold (thread stride, wave butterfly, waves in order)
+  static_assert(PRL_MAX_SEG == 4, "one double2 pair per partial row");
+  double acc[PRL_MAX_SEG] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) {
+    const double2 lo = reinterpret_cast<const double2*>(part + (size_t)b * PRL_MAX_SEG)[0];
+    const double2 hi = reinterpret_cast<const double2*>(part + (size_t)b * PRL_MAX_SEG)[1];
+    acc[0] += lo.x; acc[1] += lo.y; acc[2] += hi.x; acc[3] += hi.y;
+  }
+  __shared__ double red4[ADAM_THREADS / 64][PRL_MAX_SEG];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int s = 0; s < PRL_MAX_SEG; s++) {
+      const double v = wave_sum_d(acc[s]);
+      if (lane == 0) red4[w][s] = v;
     }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < sg.n) {  // thread s: segment s's clip coefficient and Adam step size
+    const int s = threadIdx.x;
+    double tot = 0.0;
+    for (int w = 0; w < ADAM_THREADS / 64; w++) tot += red4[w][s];  // waves in order
+    const float norm = (float)sqrt(tot);
+    coef[s] = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
+    const double t = (double)step[s];
+    const double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
+    ssz[s] = (float)((double)lr[s] / bc1);
+    ibc2[s] = (float)(1.0 / sqrt(bc2));
   }
   __syncthreads();
   auto upd = [&](int64_t i, float gv, float mv, float vv, float pv) {
@@ -820,7 +840,7 @@ int prl_mlp_step_norm_parts(const prl_net* nets, int sdim, int B) {
   float dummy;
   size_t wf = 0;
   if (!nets || B <= 0 || sdim <= 0 || mlp_layout(nets, sdim, B, nullptr, &dummy, &a, &g, &wf)) return 0;
-  return ((g.ntw + g.rfirst[g.ne] + mlp::GWV - 1) / mlp::GWV) * mlp::GWV;
+  return (g.ntw + g.rfirst[g.ne] + mlp::GWV - 1) / mlp::GWV;  // the gradient kernel's workgroups
 }
 
 }  // extern "C"
@@ -894,8 +914,8 @@ int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int 
       g.e[e].seg = g.e[e].dst == log_row ? -1 : seg_of(g.e[e].dst);
       if (g.e[e].dst != log_row && g.e[e].seg < 0) return fail("prl_mlp_step_idx_norm: a gradient outside the segments");
     }
-    const int waves = ((g.ntw + g.rfirst[g.ne] + mlp::GWV - 1) / mlp::GWV) * mlp::GWV;
-    if (no->nparts < waves) return fail("prl_mlp_step_idx_norm: partial buffer too small (prl_mlp_step_norm_parts)");
+    const int blocks = (g.ntw + g.rfirst[g.ne] + mlp::GWV - 1) / mlp::GWV;
+    if (no->nparts < blocks) return fail("prl_mlp_step_idx_norm: partial buffer too small (prl_mlp_step_norm_parts)");
     g.npart = no->part;
     g.adam_step = no->adam_step;
     g.nseg = no->nseg;

@@ -154,7 +154,7 @@ int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float*
                      void* stream);
 /* prl_mlp_step_idx that also leaves the clip_grad_norm_ partials for prl_clip_adam_parts (one
  * launch less per minibatch): grad_base = the flat gradient buffer the layers' gradients live
- * in, seg_end[nseg] its segments (as prl_clip_adam); the gradient kernel writes each wave's sum
+ * in, seg_end[nseg] its segments (as prl_clip_adam); the gradient kernel writes each workgroup's sum
  * of squares per segment into norm_part [nparts][PRL_MAX_SEG] f64 (nparts >=
  * prl_mlp_step_norm_parts) and advances adam_step[nseg] (the optimisers' step counts) by one. */
 int prl_mlp_step_norm_parts(const prl_net* nets, int sdim, int B);
