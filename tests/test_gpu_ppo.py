@@ -350,3 +350,36 @@ def test_chunked_graph_update_equals_eager(ppo, tmp_path):
     np.testing.assert_array_equal(agents[0].last_update_log.cpu().numpy(), agents[1].last_update_log.cpu().numpy())
     for (k, p0), (_, p1) in zip(_params(agents[0]).items(), _params(agents[1]).items()):
         np.testing.assert_array_equal(p0.cpu().numpy(), p1.cpu().numpy(), err_msg=k)
+
+
+def test_fused_norm_partials_equal_norm_pass(ppo, tmp_path, monkeypatch):
+    """clip_grad_norm_ from the gradient kernel's per-workgroup partials (one clip+Adam launch,
+    the default) against the separate grad_sumsq pass (PIANORL_SUMSQ=1): the same f64 norm up to
+    summation order, so parameters and logs agree to fp32 rounding after two update() calls."""
+    rng = np.random.RandomState(12)
+    n, S, B = 200, 64, 32
+    s = rng.rand(n, S).astype(np.float32)
+    a = rng.uniform(-1, 1, (n, 45)).astype(np.float32)
+    lp = rng.uniform(-60, -40, n).astype(np.float32)
+    r, d = rng.rand(n), (rng.rand(n) < 0.1).astype(np.float32)
+    ns = rng.rand(n, S).astype(np.float32)
+    agents = []
+    for sumsq in (False, True):
+        if sumsq:
+            monkeypatch.setenv("PIANORL_SUMSQ", "1")
+        else:
+            monkeypatch.delenv("PIANORL_SUMSQ", raising=False)
+        torch.manual_seed(0)
+        ag = ppo.PPOAgent(S, 45, batch_size=B, ppo_epochs=2, use_wandb=False, checkpoint_dir=str(tmp_path),
+                          graphs=False)
+        ag.critic.eval()
+        for call in range(2):
+            torch.manual_seed(200 + call)
+            ag.update(s, a, r, lp, ns, d)
+        assert ag._fused is not None and ag._fused.fused_norm == (not sumsq)
+        agents.append(ag)
+    np.testing.assert_allclose(agents[0].last_update_log.cpu().numpy(), agents[1].last_update_log.cpu().numpy(),
+                               rtol=1e-5, atol=1e-6)
+    for (k, p0), (_, p1) in zip(_params(agents[0]).items(), _params(agents[1]).items()):
+        q0, q1 = p0.cpu().numpy(), p1.cpu().numpy()
+        np.testing.assert_allclose(q0, q1, rtol=0, atol=1e-6 * max(np.abs(q1).max(), 1e-6), err_msg=k)
