@@ -3,7 +3,11 @@
 One "step" = one control step (0.05 s of simulated time = 10 physics substeps + task
 layer) of every env on every GPU, random uniform canonical actions (pre-generated on
 device with torch's Philox generator, seed 12345 + rank). Inputs and state are resident in
-HBM when the timed region starts. Multi-GPU: one process per GPU, 4096 envs per GPU
+HBM when the timed region starts. The timed hand is the reference's default PianoTask collider
+set (--hand hull: primitive_fingertip_collisions=False, palm boxes + convex-hull distal
+colliders); the same workload with the reference's primitive option (palm boxes + capsule distal
+colliders) and with the all-capsule authored hand follows as the line's "primitive_fingertips"
+and "capsule_hand" legs. Multi-GPU: one process per GPU, 4096 envs per GPU
 (weak scaling, envs shard with no data-path collective); episode returns are gathered
 over RCCL after the timed region for logging.
 
@@ -35,6 +39,15 @@ def bytes_per_env_step(obs_dim):
     + obs write + reward/discount/step_type 12 = 4884 B (obs 329) / 4844 B (obs 319)."""
     return 45 * 4 + 3 * 140 * 4 * 2 + 16 + obs_dim * 4 + 12
 
+# collider sets: TaskConfig.primitive_fingertip_collisions value, kernel instantiation, description
+HANDS = {
+    "hull": (False, "pianosim_kernel<true>", "palm boxes + convex-hull distal colliders: the reference's default "
+                                             "PianoTask(primitive_fingertip_collisions=False)"),
+    "primitive": (True, "pianosim_kernel<true>", "palm boxes + capsule distal colliders: the reference's "
+                                                 "PianoTask(primitive_fingertip_collisions=True)"),
+    "authored": (None, "pianosim_kernel<false>", "all-capsule authored hand (no reference counterpart)"),
+}
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector), spec
 
@@ -46,14 +59,17 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
     p.add_argument("--song", default="crossing_field", choices=["twinkle", "crossing_field", "guren"])
-    p.add_argument("--hand", default="authored", choices=["authored", "hull"],
-                   help="authored: capsule colliders (primitive_fingertip_collisions=True); hull: palm boxes "
-                        "and convex-hull fingertips, the reference's default collider kinds (shadow_hand.py:95,144-152)")
+    p.add_argument("--hand", default="hull", choices=list(HANDS),
+                   help="collider set of the timed workload: hull = the reference's default "
+                        "(PianoTask(primitive_fingertip_collisions=False): palm boxes + convex-hull distal "
+                        "colliders, shadow_hand.py:95,144-152, tasks/base.py:101); primitive = the reference's "
+                        "primitive_fingertip_collisions=True (palm boxes + capsule distal colliders); authored = "
+                        "the all-capsule hand (no reference counterpart)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-hull-leg", action="store_true",
-                   help="skip timing the same workload with the box / hull hand after the main line")
+    p.add_argument("--no-legs", "--no-hull-leg", dest="no_legs", action="store_true",
+                   help="skip timing the same workload with the other two collider sets after the main line")
     p.add_argument("--cpu-sample-envs", type=int, default=16)
-    p.add_argument("--cpu-sample-steps", type=int, default=1000)
+    p.add_argument("--cpu-sample-steps", type=int, default=500)
     return p.parse_args()
 
 
@@ -295,10 +311,12 @@ def main():
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
     seq, task = load_song(dp, args.song)
     import dataclasses
-    if args.hand == "hull":  # the reference's default colliders (shadow_hand.py:95,144-152)
-        task = dataclasses.replace(task, primitive_fingertip_collisions=False)
+
+    def hand_task(hand):  # TaskConfig of a collider set (HANDS)
+        return dataclasses.replace(task, primitive_fingertip_collisions=HANDS[hand][0])
+
     shard = sharding.shard_envs(args.envs * world, rank, world)  # weak scaling: envs per GPU fixed
-    env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
+    env = dp.BatchedPianoEnv(shard.count, seq, hand_task(args.hand), device=dev, seed=12345,
                              env_offset=shard.start)
     N = shard.count
     gen = torch.Generator(device=dev).manual_seed(12345 + rank)
@@ -318,24 +336,24 @@ def main():
     obs_dim = env.obs_dim
     total_steps = args.envs * world * args.steps
     value = total_steps / elapsed
-    hull_leg = None
-    if args.hand == "authored" and not args.no_hull_leg:
-        # the same workload with the reference's default colliders (primitive_fingertip_collisions
-        # =False: palm boxes, convex-hull fingertips; the box / hull kernel instantiation), after
-        # the main timed region: same envs, actions, K and W
-        env.close()
-        henv = dp.BatchedPianoEnv(shard.count, seq, dataclasses.replace(task, primitive_fingertip_collisions=False),
-                                  device=dev, seed=12345, env_offset=shard.start)
-        henv.reset()
-        stagger_episodes(henv, shard.start, henv.song.T)
-        h_elapsed, h_kernel_ms = timed_rollout(henv, actions, args.steps, args.warmup, dev,
-                                               sharding.EpisodeReturns(N, dev), sharding)
-        hull_leg = {"value": total_steps / h_elapsed, "ms_per_step": h_elapsed / args.steps * 1e3,
-                    "kernel_ms_avg": h_kernel_ms, "unit": "env-steps/s",
-                    "hand": "palm boxes + convex-hull fingertips (TaskConfig(primitive_fingertip_collisions=False), "
-                            "the reference's default; pianosim_kernel<true>)"}
-        henv.close()
-        env = None
+    env.close()
+    env = None
+    legs = {}
+    if not args.no_legs:
+        # the same workload (envs, actions, K, W) with the other collider sets, after the main
+        # timed region; top-level keys of the line (the driver's parsed record keeps them)
+        for hand in HANDS:
+            if hand == args.hand:
+                continue
+            lenv = dp.BatchedPianoEnv(shard.count, seq, hand_task(hand), device=dev, seed=12345, env_offset=shard.start)
+            lenv.reset()
+            stagger_episodes(lenv, shard.start, lenv.song.T)
+            l_elapsed, l_kernel_ms = timed_rollout(lenv, actions, args.steps, args.warmup, dev,
+                                                   sharding.EpisodeReturns(N, dev), sharding)
+            legs[hand] = {"value": total_steps / l_elapsed, "ms_per_step": l_elapsed / args.steps * 1e3,
+                          "kernel_ms_avg": l_kernel_ms, "unit": "env-steps/s", "hand": HANDS[hand][2],
+                          "kernel": HANDS[hand][1]}
+            lenv.close()
     if rank == 0:
         sha = lib_sha()
         bpe = bytes_per_env_step(obs_dim)
@@ -359,8 +377,7 @@ def main():
                                    f"per env-step, constraint forces by the primal Newton solve (friction loss, "
                                    f"uncapped rows)",
                        "envs_per_gpu": N, "song": args.song, "parallelism": f"dp{world}",
-                       "hand": args.hand + (" (capsule colliders)" if args.hand == "authored" else
-                                            " (palm boxes + convex-hull fingertips, pianosim_kernel<true>)"),
+                       "hand": f"{args.hand}: {HANDS[args.hand][2]}",
                        "mean_return_logged": mean_ret, "episodes_finished": fin_n,
                        "per_env_returns_gathered": int(per_env.numel()),
                        "mean_last_episode_return": float(per_env_done.mean()) if per_env_done.numel() else None,
@@ -371,11 +388,10 @@ def main():
                                             "max_contact_rows": int(stats[:, 3].max()),
                                             "coupled_substep_frac": float(stats[:, 4].sum() / (10.0 * stats.shape[0])),
                                             "bad_pivot_substeps": int(stats[:, 5].sum()),
-                                            "max_coupled_dofs": int(stats[:, 6].max())},
-                       "hull_hand": hull_leg},
+                                            "max_coupled_dofs": int(stats[:, 6].max())}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "pianosim_kernel", "kernel_ms_avg": kernel_ms,
+                         "kernel": HANDS[args.hand][1], "kernel_ms_avg": kernel_ms,
                          "kernel_ms_note": "HIP events around ps_step on the launch stream: order_kernel "
                                            "(counting sort, ~5 us) + pianosim_kernel",
                          "bytes_per_env_step": bpe, "wave_time": issue_summary(N, args.song, sha, args.hand),
@@ -384,11 +400,16 @@ def main():
             "valu_roofline": valu_roofline(args.song, N, kernel_ms),
             "qpos_drift": drift_summary(sha),
         }
+        # the other collider sets on the same workload (reference primitive option; all-capsule hand)
+        if "primitive" in legs:
+            line["primitive_fingertips"] = legs["primitive"]
+        if "authored" in legs:
+            line["capsule_hand"] = legs["authored"]
+        if "hull" in legs:
+            line["reference_default_hand"] = legs["hull"]
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
-            line["cpu_baseline"] = cpu_baseline(dp, seq, task, args.cpu_sample_envs, args.cpu_sample_steps)
+            line["cpu_baseline"] = cpu_baseline(dp, seq, hand_task(args.hand), args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(line), flush=True)
-    if env is not None:
-        env.close()
     if world > 1:
         dist.destroy_process_group()
 

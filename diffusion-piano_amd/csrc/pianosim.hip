@@ -344,6 +344,11 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
         m->dof_act_coef[dofs[i]] = cs[i];
       }
     }
+  // every action column before the sustain pedal drives an actuator: a gap would be an input the
+  // kernel ignores while ps_env_action_dim reports it
+  if (__builtin_popcountll(cols) != m->n_action - 1)
+    return fail("act_column must fill columns 0 .. n_action - 2 (" + std::to_string(__builtin_popcountll(cols)) +
+                " actuator columns for n_action " + std::to_string(m->n_action) + ")");
   // geoms, sites, pairs
   for (int h = 0; h < NH; h++)
     for (int g = 0; g < NG; g++) {

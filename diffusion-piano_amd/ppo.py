@@ -887,7 +887,7 @@ class RolloutTrainer:
         f32 = dict(device=env.device, dtype=torch.float32)
         H = 1 if reference_semantics else horizon
         self.obs = torch.empty(H, N, D, **f32)
-        self.act = torch.empty(H, N, 45, **f32)
+        self.act = torch.empty(H, N, env.action_dim, **f32)  # the model's action row (39 / 41 / 43 / 45)
         self.logp = torch.empty(H, N, **f32)
         self.rew = torch.empty(H, N, **f32)
         self.done = torch.empty(H, N, **f32)

@@ -58,12 +58,16 @@ class EpisodeReturns:
             from . import _lib
             L = _lib.load()
             if hasattr(L, "ps_episode_returns"):
-                st = step_type if step_type.dtype == torch.uint8 else step_type.to(torch.uint8)
-                rew = reward if reward.dtype == torch.float32 else reward.to(torch.float32)
-                _lib.check(L.ps_episode_returns(rew.data_ptr(), st.contiguous().data_ptr(), self.running.numel(),
-                                                self.running.data_ptr(), self.last_return.data_ptr(),
-                                                self.finished_sum.data_ptr(), self.finished_count.data_ptr(),
-                                                torch.cuda.current_stream().cuda_stream))
+                dev = self.running.device
+                st = step_type.to(device=dev, dtype=torch.uint8).contiguous()
+                rew = reward.to(device=dev, dtype=torch.float32).contiguous()
+                # launched on the buffers' device and its current stream, whatever the caller's
+                # current device is (several GPUs in one process)
+                with torch.cuda.device(dev):
+                    _lib.check(L.ps_episode_returns(rew.data_ptr(), st.data_ptr(), self.running.numel(),
+                                                    self.running.data_ptr(), self.last_return.data_ptr(),
+                                                    self.finished_sum.data_ptr(), self.finished_count.data_ptr(),
+                                                    torch.cuda.current_stream(dev).cuda_stream))
                 return
         first = step_type == 0
         self.running = torch.where(first, torch.zeros_like(self.running), self.running + reward.to(torch.float64))

@@ -21,6 +21,15 @@ def song(dp, name):
     raise KeyError(name)
 
 
+def tool_hand_kwargs():
+    """TaskConfig kwargs of the collider set a development tool runs (PIANOSIM_HAND = hull |
+    primitive | authored, bench.py --hand; PIANOSIM_HULL=1 = hull; default the all-capsule hand)."""
+    import os
+    h = os.environ.get("PIANOSIM_HAND") or ("hull" if os.environ.get("PIANOSIM_HULL") else "authored")
+    return {"hull": {"primitive_fingertip_collisions": False}, "primitive": {"primitive_fingertip_collisions": True},
+            "authored": {}}[h]
+
+
 def random_states(md, n, rng, vscale=0.5):
     """Random joint configurations inside the ranges (keys slightly beyond, to hit limits)."""
     q = np.zeros((n, 140))
@@ -56,16 +65,23 @@ def perturbed(state, rng, scale=1e-7):
     return s
 
 
-def assert_parity(e, floor, what="", tol=1e-4, well=1e-5):
+# absolute ceilings of the all-sample clause (a gate relative to the checker's own
+# sensitivity alone is unbounded where that sensitivity is large)
+PARITY_P99_CEIL = 2e-4
+PARITY_MAX_CEIL = 1e-2
+
+
+def assert_parity(e, floor, what="", tol=1e-4, well=1e-5, p99_ceil=PARITY_P99_CEIL, max_ceil=PARITY_MAX_CEIL):
     """The parity gate of a teacher-forced comparison (fp32 kernel vs fp64 checker, one control
     step from the same state), per env-step qpos L-inf error `e` and the checker's own
     sensitivity `floor` (the same step from the state moved by ``perturbed``):
       * median < 1e-5;
-      * p99 < tol over the well-conditioned env-steps (floor < well; most of them);
-      * p99 over all env-steps within max(tol, 2x the floor's p99): the ill-conditioned ones - a
-        contact starting or ending at near-zero distance, where the soft contact's force steps -
-        move the checker itself by more than tol under a 1e-7 rad perturbation, so no
-        implementation that is not bit-identical to it stays below tol there."""
+      * p99 < tol over the well-conditioned env-steps (floor < well; at least half of them);
+      * p99 over all env-steps within max(tol, 2x the floor's p99) - the ill-conditioned ones (a
+        contact starting or ending at near-zero distance, a stick-slip flip) move the checker
+        itself by more than tol under a 1e-7 rad perturbation - and never above the absolute
+        ceiling p99_ceil; the largest error at most max_ceil.
+    Returns the summary (with the floor's p99, so a loosened gate shows in the logs)."""
     e, floor = np.asarray(e, np.float64), np.asarray(floor, np.float64)
     calm = floor < well
     msg = (f"{what}: n {e.size}, median {np.median(e):.2e}, p99 {np.percentile(e, 99):.2e}, max {e.max():.2e}; "
@@ -75,5 +91,6 @@ def assert_parity(e, floor, what="", tol=1e-4, well=1e-5):
     assert np.median(e) < 1e-5, msg
     assert calm.sum() >= 0.5 * e.size, msg
     assert np.percentile(e[calm], 99) < tol, msg
-    assert np.percentile(e, 99) <= max(tol, 2.0 * np.percentile(floor, 99)), msg
+    assert np.percentile(e, 99) <= min(max(tol, 2.0 * np.percentile(floor, 99)), p99_ceil), msg
+    assert e.max() <= max_ceil, msg
     return msg

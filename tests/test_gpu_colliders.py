@@ -71,6 +71,8 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
             for kind, key, g1, g2, dist in o.contacts(i):
                 kinds.add((kind, g1 >= 40, g2 >= 40))
     e, f = np.concatenate(errs), np.concatenate(floor)
+    print(f"box/hull hand: qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}; "
+          f"1e-6 rad floor median {np.median(f):.2e} p99 {np.percentile(f, 99):.2e}")
     assert np.median(e) < 1e-5, (np.median(e), np.median(f))
     assert np.percentile(e, 99) <= max(5e-4, 2 * np.percentile(f, 99)), (np.percentile(e, 99), np.percentile(f, 99))
     re, rf = np.concatenate(rerr), np.concatenate(rfloor)
@@ -79,6 +81,48 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
     assert same > 0.9, same
     # the run exercised hull-key, box/hull-capsule and box/hull-box/hull pairs
     assert (0, False, True) in kinds and (2, True, False) in kinds and (2, True, True) in kinds, kinds
+
+
+def test_box_hull_hand_one_substep(dp, ref):
+    """The reference's default colliders (palm boxes, hull fingertips) at the one-substep gate:
+    GPU vs checker for ONE physics substep from the same states (rollout states of the GPU under
+    random actions), where the contact set and the MPR portals come from the same positions and
+    nothing compounds: qpos median < 1e-6, p99 < 5e-5, qvel (qacc h) relative p99 < 1e-3."""
+    n = 64
+    seq = song(dp, "twinkle")
+    task1 = dp.TaskConfig(primitive_fingertip_collisions=False, control_timestep=0.005)
+    task10 = dp.TaskConfig(primitive_fingertip_collisions=False)
+    md, st, tc = dp.compile_task(seq, task1, canonical_actions=False)
+    assert md.n_substeps == 1
+    roll = dp.BatchedPianoEnv(n, seq, task10, device="cuda:0", canonical_actions=False)
+    g = dp.BatchedPianoEnv(n, seq, task1, device="cuda:0", canonical_actions=False)
+    o = ref.OracleEnv(md, st, tc, n)
+    lo, hi = dp.model.action_spec(md)
+    rng = np.random.RandomState(6)
+    roll.reset()
+    eq, ea, ncon = [], [], 0
+    for t in range(12):
+        roll.step(torch.from_numpy(rng.uniform(lo, hi, (n, 45)).astype(np.float32)).cuda())
+        s = {k: v for k, v in _gs(roll).items() if k in KEYS}
+        a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
+        g.set_state(s)
+        o.set_state(s)
+        g.step(torch.from_numpy(a).cuda())
+        o.step(a)
+        sg, so = _gs(g), o.get_state()
+        eq.append(np.abs(sg["qpos"] - so["qpos"]).max(axis=1))
+        v0 = s["qvel"].astype(np.float64)
+        acc_o, acc_g = (so["qvel"] - v0) / 0.005, (sg["qvel"] - v0) / 0.005
+        ea.append(np.abs(acc_g - acc_o).max(axis=1) / np.maximum(np.abs(acc_o).max(axis=1), 1.0))
+        ncon += int(o.contact_count().sum())
+    eq, ea = np.concatenate(eq), np.concatenate(ea)
+    msg = (f"box/hull hand, one substep: {ncon} contacts; qpos err median {np.median(eq):.2e} p99 "
+           f"{np.percentile(eq, 99):.2e} max {eq.max():.2e}; qacc rel err median {np.median(ea):.2e} p99 "
+           f"{np.percentile(ea, 99):.2e} max {ea.max():.2e}")
+    print(msg)
+    assert ncon > 0
+    assert np.median(eq) < 1e-6 and np.percentile(eq, 99) < 5e-5, msg
+    assert np.percentile(ea, 99) < 1e-3, msg
 
 
 def test_box_hull_hand_duplicates_bitwise(dp, task):

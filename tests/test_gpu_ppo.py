@@ -186,6 +186,27 @@ def test_rollout_trainer_on_env(ppo, reference_semantics, tmp_path):
     env.close()
 
 
+@pytest.mark.parametrize("reference_semantics", [True, False])
+def test_rollout_trainer_reduced_action_space(ppo, reference_semantics, tmp_path):
+    """The loop on a model whose action row is not 45 wide: reduced_action_space
+    gives 2 x 19 actuators + sustain = 39 columns (shadow_hand_test.py:89-99); the agent and the
+    trainer's action buffer take env.action_dim."""
+    dp = importlib.import_module("diffusion-piano_amd")
+    env = dp.BatchedPianoEnv(64, dp.music.twinkle_twinkle_little_star_one_hand(),
+                             dp.TaskConfig(reduced_action_space=True), device="cuda:0")
+    assert env.action_dim == 39
+    torch.manual_seed(0)
+    agent = ppo.PPOAgent(env.obs_dim, env.action_dim, batch_size=128, ppo_epochs=2, checkpoint_dir=str(tmp_path),
+                         use_wandb=False)
+    tr = ppo.RolloutTrainer(env, agent, horizon=4, reference_semantics=reference_semantics)
+    assert tr.act.shape[-1] == 39
+    steps = sum(tr.iterate() for _ in range(2))
+    assert steps == 64 * (2 if reference_semantics else 8)
+    assert torch.isfinite(agent.last_update_log).all()
+    assert torch.isfinite(tr.ep_return).all()
+    env.close()
+
+
 def _fused_agent(ppo, z, tmp_path, mfma, train_critic, batch):
     ag = _agent(ppo, z, tmp_path, graphs=False)
     ag.fused = True
@@ -383,3 +404,33 @@ def test_fused_norm_partials_equal_norm_pass(ppo, tmp_path, monkeypatch):
     for (k, p0), (_, p1) in zip(_params(agents[0]).items(), _params(agents[1]).items()):
         q0, q1 = p0.cpu().numpy(), p1.cpu().numpy()
         np.testing.assert_allclose(q0, q1, rtol=0, atol=1e-6 * max(np.abs(q1).max(), 1e-6), err_msg=k)
+
+
+def test_fused_norm_partials_per_segment(ppo, tmp_path):
+    """The gradient kernel's clip-norm partials themselves (Adam barely moves under a
+    constant gradient scale, so parameters alone would not catch a dropped segment): summed over
+    the partial rows, each optimiser segment's partial equals the f64 sum of squares of that
+    segment of the flat gradient the same launch wrote, to 1e-12 relative."""
+    rng = np.random.RandomState(13)
+    n, S, B = 96, 64, 32
+    batch = (rng.rand(n, S).astype(np.float32), rng.uniform(-1, 1, (n, 45)).astype(np.float32), rng.rand(n),
+             rng.uniform(-60, -40, n).astype(np.float32), rng.rand(n, S).astype(np.float32),
+             (rng.rand(n) < 0.1).astype(np.float32))
+    torch.manual_seed(0)
+    ag = ppo.PPOAgent(S, 45, batch_size=B, ppo_epochs=1, use_wandb=False, checkpoint_dir=str(tmp_path), graphs=False)
+    ag.critic.train()
+    ag._prepare(*batch)
+    ag._fused = ppo.FusedStep(ag)
+    assert ag._fused.fused_norm and ag._fused._mlp_ok(B)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(3))[:B].cuda()
+    ag._fused(idx)
+    torch.cuda.synchronize()
+    parts = ag._fused.bufs[B]["_norm_part"].sum(0).cpu().numpy()
+    fl = ag.flat
+    ends = [int(x) for x in fl.seg_end]
+    g = fl.flat.double().cpu().numpy()
+    for s, (a, b) in enumerate(zip([0] + ends[:-1], ends)):
+        ref = float(np.sum(g[a:b] ** 2))
+        assert ref > 0.0, s
+        assert abs(parts[s] - ref) <= 1e-12 * ref, (s, parts[s], ref)
+    assert np.all(parts[fl.nseg:] == 0.0)

@@ -10,7 +10,7 @@ sensitivity's p99) - on the bench song, the replays of coupled-hand and heavy-co
 import numpy as np
 import pytest
 
-from helpers import assert_parity, perturbed, song
+from helpers import PARITY_MAX_CEIL, PARITY_P99_CEIL, assert_parity, perturbed, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -146,20 +146,11 @@ def test_newton_coupled_hands_full_block(dp, ref, monkeypatch):
     assert_parity(e, f, "coupled env-steps, whole C block")
 
 
-def test_newton_whole_c_block_overlapping_hands(dp, ref):
+def _overlap_states(md, rng):
     """The right hand slid along the keyboard (forearm_tx) and raised (forearm_ty) onto the left
-    one: hand-hand contacts across many fingers couple more than 28 dofs of both hands
-    (PS_STAT_MAX_CDOFS), which the 16-column C block cannot hold, so the whole-block solve (both
-    hands' C blocks in slot layout) runs. Overlapping hands are mostly violent (explosive contact
-    forces: the checker itself moves by ~1e-2 under a 1e-7 rad perturbation of the joints), so
-    the GPU is held to the checker's own sensitivity there (median within the sensitivity's
-    median, p99 within 2x its p99), and to the parity gate (median < 1e-5, p99 < 1e-4) on the
-    states whose sensitivity is below 1e-5; one control step from the same state."""
-    seq = song(dp, "crossing_field")
-    task = dp.TaskConfig(trim_silence=True)
-    md, sttab, tc = dp.compile_task(seq, task, canonical_actions=False)
+    one, every position actuator held at its joint: hand-hand contacts across many fingers
+    couple more than 28 dofs of both hands. -> (state dict, actions)."""
     lo, hi = dp_action_spec(md)
-    rng = np.random.RandomState(11)
     # side by side (forearm_tx), and the right hand raised (forearm_ty) over the left one: flat
     # hands stacked at the height where they touch along the fingers
     grid = [(tx, ty) for tx in np.linspace(-0.30, -0.12, 37) for ty in (0.0, 0.02, 0.04, 0.06)]
@@ -187,6 +178,24 @@ def test_newton_whole_c_block_overlapping_hands(dp, ref):
     st = {"qpos": q.astype(np.float32), "qvel": np.zeros((N, 140), np.float32),
           "qacc_ws": np.zeros((N, 140), np.float32), "ctrl": np.zeros((N, 44), np.float32),
           "sustain": np.zeros(N, np.float32), "t_idx": np.full(N, 5, np.int32), "last": np.zeros(N, np.uint8)}
+    return st, a
+
+
+def test_newton_whole_c_block_overlapping_hands(dp, ref):
+    """The right hand slid along the keyboard (forearm_tx) and raised (forearm_ty) onto the left
+    one: hand-hand contacts across many fingers couple more than 28 dofs of both hands
+    (PS_STAT_MAX_CDOFS), which the 16-column C block cannot hold, so the whole-block solve (both
+    hands' C blocks in slot layout) runs. Overlapping hands are mostly violent (explosive contact
+    forces: the checker itself moves by ~1e-2 under a 1e-7 rad perturbation of the joints), so
+    the GPU is held to the checker's own sensitivity there (median within the sensitivity's
+    median, p99 within 2x its p99), and to the parity gate (median < 1e-5, p99 < 1e-4) on the
+    states whose sensitivity is below 1e-5; one control step from the same state."""
+    seq = song(dp, "crossing_field")
+    task = dp.TaskConfig(trim_silence=True)
+    md, sttab, tc = dp.compile_task(seq, task, canonical_actions=False)
+    rng = np.random.RandomState(11)
+    st, a = _overlap_states(md, rng)
+    N = len(a)
     g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", canonical_actions=False)
     g.set_state(st)
     g.step(torch.from_numpy(a).cuda())
@@ -217,6 +226,98 @@ def test_newton_whole_c_block_overlapping_hands(dp, ref):
     if calm.any():
         ec = e[calm]
         assert np.median(ec) < 1e-5 and np.percentile(ec, 99) < 1e-4, (np.median(ec), np.percentile(ec, 99), ec.max())
+
+
+def _one_substep(dp, ref, st, a, select, **kw):
+    """One physics substep (control_timestep = the physics timestep) from the same states on the
+    GPU and the checker, on the states whose GPU solver counters `select` picks (no physics
+    warning). -> (GPU counters of the picked states, qpos L-inf error, qacc L-inf error relative
+    to the checker's largest |qacc|, at least 1)."""
+    seq = song(dp, "crossing_field")
+    task = dp.TaskConfig(trim_silence=True, control_timestep=0.005, **kw)
+    md, sttab, tc = dp.compile_task(seq, task, canonical_actions=False)
+    assert md.n_substeps == 1
+    N = len(a)
+    g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", canonical_actions=False)
+    g.set_state(st)
+    g.step(torch.from_numpy(a).cuda())
+    stats = g.solver_stats().cpu().numpy()
+    warn = g.warnings().cpu().numpy()
+    pick = np.nonzero(select(stats) & (warn.sum(1) == 0))[0]
+    if not len(pick):
+        return stats[pick], np.zeros(0), np.zeros(0)
+    sub = {k: np.asarray(x)[pick] for k, x in st.items()}
+    o = ref.OracleEnv(md, sttab, tc, len(pick))
+    o.set_state(sub)
+    o.step(a[pick])
+    so = o.get_state()
+    sg = {k: v.cpu().numpy()[pick] for k, v in g.get_state().items()}
+    eq = np.abs(sg["qpos"] - so["qpos"]).max(axis=1)
+    v0 = np.asarray(sub["qvel"], np.float64)
+    h = float(md.timestep)
+    acc_o, acc_g = (so["qvel"] - v0) / h, (sg["qvel"].astype(np.float64) - v0) / h
+    ea = np.abs(acc_g - acc_o).max(axis=1) / np.maximum(np.abs(acc_o).max(axis=1), 1.0)
+    return stats[pick], eq, ea
+
+
+def test_one_substep_whole_c_block(dp, ref):
+    """the whole-C-block template (more than 28 coupled dofs of both hands) held to
+    the one-substep gate - one substep is far better conditioned than a control step (no 10-fold
+    compounding through the soft contacts), so the fp32 solve is measured, not the chaos: qpos
+    median < 1e-6, p99 < 5e-5 (test_gpu_parity.py's substep gate), qacc relative to the largest
+    |qacc| p99 < 1e-3. The GPU counters must show the path: more than 28 coupled dofs."""
+    md = dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True), canonical_actions=False)[0]
+    st, a = _overlap_states(md, np.random.RandomState(11))
+    stats, eq, ea = _one_substep(dp, ref, st, a, lambda s: (s[:, 6] > 28) & (s[:, 1] == 0))
+    msg = (f"{len(eq)} states, coupled dofs max {stats[:, 6].max() if len(eq) else 0}: qpos err median "
+           f"{np.median(eq):.2e} p99 {np.percentile(eq, 99):.2e} max {eq.max():.2e}; qacc rel err median "
+           f"{np.median(ea):.2e} p99 {np.percentile(ea, 99):.2e} max {ea.max():.2e}")
+    print(msg)
+    assert len(eq) >= 8 and stats[:, 6].max() > 28, msg
+    assert np.median(eq) < 1e-6 and np.percentile(eq, 99) < 5e-5, msg
+    assert np.percentile(ea, 99) < 1e-3, msg
+
+
+def _contact_rich_states(dp, ref, n=4096, seed=7):
+    """Random hand poses pushed toward flexion (the upper 40% of every joint range), one control
+    step of the checker to settle the initial penetrations (max_contacts 24). -> (state, actions)."""
+    from helpers import random_states
+    task = dict(trim_silence=True, max_contacts=24)
+    md, st, tc = dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(**task), canonical_actions=False)
+    rng = np.random.RandomState(seed)
+    o = ref.OracleEnv(md, st, tc, n)
+    o.reset()
+    s0 = o.get_state()
+    q, v = random_states(md, n, rng)
+    lo = np.array([md.dof_range[h][j][0] for h in range(2) for j in range(26)])
+    hi = np.array([md.dof_range[h][j][1] for h in range(2) for j in range(26)])
+    q[:, 88:] = lo + (hi - lo) * rng.uniform(0.6, 1.0, (n, 52))
+    s0["qpos"], s0["qvel"] = q, v * 0.0
+    la, ha = dp_action_spec(md)
+    a = np.repeat(((la + ha) / 2)[None], n, 0).astype(np.float32)
+    o.set_state(s0)
+    o.step(a)  # settle
+    return md, st, tc, o, a
+
+
+def test_one_substep_full_contact_capacity(dp, ref):
+    """states at 22-24 contacts in the substep (max_contacts 24 = MAXCON; 88+ contact
+    rows, the contact lanes past 64 direction rows) held to the one-substep gate: qpos median
+    < 1e-6, p99 < 5e-5; qacc relative p99 < 1e-3. The GPU counters must show the path: 88 or
+    more contact rows (PS_STAT_MAX_ROWS = 4 x contacts) in the picked states."""
+    md, sttab, tc, o, a = _contact_rich_states(dp, ref)
+    s1 = o.get_state()
+    cand = np.nonzero(o.contact_count() >= 21)[0]
+    assert len(cand) >= 8, f"only {len(cand)} states with >= 21 contacts"
+    states = {k: np.asarray(s1[k])[cand] for k in KEYS}
+    stats, eq, ea = _one_substep(dp, ref, states, a[cand], lambda s: s[:, 3] >= 88, max_contacts=24)
+    msg = (f"{len(eq)} of {len(cand)} states at >= 22 contacts on the GPU (rows max {stats[:, 3].max() if len(eq) else 0}): "
+           f"qpos err median {np.median(eq) if len(eq) else 0:.2e} p99 {np.percentile(eq, 99) if len(eq) else 0:.2e}; "
+           f"qacc rel err median {np.median(ea) if len(eq) else 0:.2e} p99 {np.percentile(ea, 99) if len(eq) else 0:.2e}")
+    print(msg)
+    assert len(eq) >= 8 and stats[:, 3].min() >= 88, msg
+    assert np.median(eq) < 1e-6 and np.percentile(eq, 99) < 5e-5, msg
+    assert np.percentile(ea, 99) < 1e-3, msg
 
 
 def test_same_key_contacts_bitwise_repeatable(dp, ref):
@@ -256,34 +357,22 @@ def test_same_key_contacts_bitwise_repeatable(dp, ref):
 def test_full_contact_capacity_teacher_forced(dp, ref):
     """max_contacts = 24 (MAXCON) with 22-24 contacts in a substep: every contact's direction-row
     dots come from its own lane (a lane per direction row stopped at 64 rows = 21
-    contacts, and the 22nd+ took another contact's tangent J.v). States: random hand poses with
-    the joints pushed toward flexion, one control step of the checker to settle the initial
-    penetrations, then those still at >= 22 contacts; one teacher-forced control step, GPU vs
-    checker, gated like every other: below the checker's own 1e-7 rad sensitivity."""
-    from helpers import random_states
-    task = dict(trim_silence=True, max_contacts=24)
-    md, st, tc = dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(**task), canonical_actions=False)
-    N = 4096
-    rng = np.random.RandomState(7)
-    o = ref.OracleEnv(md, st, tc, N)
-    o.reset()
-    s0 = o.get_state()
-    q, v = random_states(md, N, rng)
-    lo = np.array([md.dof_range[h][j][0] for h in range(2) for j in range(26)])
-    hi = np.array([md.dof_range[h][j][1] for h in range(2) for j in range(26)])
-    q[:, 88:] = lo + (hi - lo) * rng.uniform(0.6, 1.0, (N, 52))
-    s0["qpos"], s0["qvel"] = q, v * 0.0
-    la, ha = dp_action_spec(md)
-    a = np.repeat(((la + ha) / 2)[None], N, 0).astype(np.float32)
-    o.set_state(s0)
-    o.step(a)  # settle
+    contacts, and the 22nd+ took another contact's tangent J.v). States: _contact_rich_states,
+    those still at >= 22 contacts after the settling step; one teacher-forced control step, GPU vs
+    checker. The GPU counters must show the >= 22-contact path in the step (88+ contact rows in
+    some substep) for at least a quarter of the states; qpos within the absolute ceiling of
+    helpers.assert_parity's all-sample clause (contact-rich states are ill-conditioned: the
+    checker moves by ~1e-3 under a 1e-7 rad perturbation; test_one_substep_full_contact_capacity
+    holds the same path to the substep gate)."""
+    md, st, tc, o, a = _contact_rich_states(dp, ref)
     pick = np.nonzero(o.contact_count() >= 22)[0]
     assert len(pick) >= 8, f"only {len(pick)} states with >= 22 contacts"
     n = len(pick)
     s1 = o.get_state()
     states = {k: np.asarray(s1[k])[pick] for k in KEYS}
     seq = song(dp, "crossing_field")
-    g = dp.BatchedPianoEnv(n, seq, dp.TaskConfig(**task), device="cuda:0", canonical_actions=False)
+    task = dp.TaskConfig(trim_silence=True, max_contacts=24)
+    g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
     o1, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
     g.reset()
     g.set_state(states)
@@ -292,16 +381,14 @@ def test_full_contact_capacity_teacher_forced(dp, ref):
     g.step(torch.from_numpy(a[:n]).cuda())
     o1.step(a[:n])
     o2.step(a[:n])
-    cg = g.contact_count().cpu().numpy()
+    rows = g.solver_stats().cpu().numpy()[:, 3]
     qo = o1.get_state()["qpos"]
     e = np.abs(g.get_state()["qpos"].cpu().numpy() - qo).max(axis=1)
     f = np.abs(o2.get_state()["qpos"] - qo).max(axis=1)
-    msg = (f"{n} states (GPU contacts at the step's last substep: median {np.median(cg):.0f}, max {cg.max()}): "
-           f"qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e}; the checker's sensitivity "
-           f"median {np.median(f):.2e} p99 {np.percentile(f, 99):.2e}")
+    msg = (f"{n} states, {int((rows >= 88).sum())} reached 88+ contact rows on the GPU (max {rows.max()}): "
+           f"qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}; the checker's "
+           f"sensitivity median {np.median(f):.2e} p99 {np.percentile(f, 99):.2e}")
     print(msg)
-    # contact-rich states are ill-conditioned (measured: error median 3.3e-5 against a checker
-    # sensitivity median of 2.7e-5, p99 3e-3 against 1.1e-2): the GPU sits at the checker's own
-    # sensitivity; a contact's rows built from another contact's dots would not
+    assert (rows >= 88).sum() >= max(4, n // 4), msg
     assert np.median(e) <= max(1e-5, 2.0 * np.median(f)), msg
-    assert np.percentile(e, 99) <= max(1e-4, 2.0 * np.percentile(f, 99)), msg
+    assert np.percentile(e, 99) <= PARITY_P99_CEIL and e.max() <= PARITY_MAX_CEIL, msg

@@ -55,3 +55,21 @@ def test_task_kwargs_teacher_forced(dp, ref, kw):
         assert locked and np.abs(q[:, locked]).max() == 0.0
     assert_parity(e, np.concatenate(fl), str(kw))
     assert np.percentile(r, 99) < 1e-3, r.max()
+
+
+def test_action_column_gap_is_rejected(dp):
+    """ps_create refuses a caller-built descriptor whose actuator columns leave a gap before the
+    sustain column: that column would be read by nobody while ps_env_action_dim
+    reports the full width."""
+    import ctypes as C
+    seq = song(dp, "twinkle")
+    task = dp.TaskConfig(reduced_action_space=True)
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    assert md.n_action == 39
+    md.n_action = 40  # columns 0..37 used, 38 unused, 39 = sustain
+    import importlib
+    lib = importlib.import_module("diffusion-piano_amd._lib").load()
+    sd = importlib.import_module("diffusion-piano_amd.abi").SongDesc.from_tables(st)
+    h = C.c_void_p()
+    rc = lib.ps_create(C.addressof(md), C.addressof(sd), C.addressof(tc), 4, 0, 1, C.byref(h))
+    assert rc < 0 and b"act_column" in lib.ps_last_error()

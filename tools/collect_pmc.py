@@ -25,9 +25,11 @@ def rows(d, pattern):
     return out
 
 
-# the profiled instantiation: pianosim_kernel<false> (capsule hand) or <true> (box / hull
-# colliders); bench.py's line also times the other one (its hull leg), which must not mix in
-KNAME = "pianosim_kernel<true>" if __import__("os").environ.get("PIANOSIM_HULL") else "pianosim_kernel<false>"
+# the profiled collider set (bench.py --hand; PIANOSIM_HAND, default the bench's default "hull") and
+# its kernel instantiation: pianosim_kernel<true> (box / hull colliders) or <false> (all-capsule
+# hand); bench.py's line also times the other sets (its legs), which must not mix in
+HAND = __import__("os").environ.get("PIANOSIM_HAND", "hull")
+KNAME = "pianosim_kernel<false>" if HAND == "authored" else "pianosim_kernel<true>"
 
 
 def counter(d, name):
@@ -55,8 +57,7 @@ def main():
     write_kb = counter(wdir, "WRITE_SIZE")
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     from bench import lib_sha  # the profiled binary (bench.py quotes only profiles of its own build)
-    import os
-    hand = "hull" if os.environ.get("PIANOSIM_HULL") else "authored"  # bench.py --hand
+    hand = HAND
     out = {"envs": envs, "song": song, "hand": hand, "kernel": KNAME, "lib_sha": lib_sha()}
     if stats:
         s = stats[0]
@@ -89,7 +90,7 @@ def main():
             w.writeheader()
             w.writerows(rows(tdir, "*kernel_stats.csv"))
     Path(f"profiles/{prefix}_pmc.json").write_text(json.dumps(out, indent=1))
-    if hand == "authored":  # the bench's default workload; the hull hand's summary stays under its prefix
+    if hand == "hull":  # the bench's default workload; the other sets' summaries stay under their prefix
         Path("profiles/pmc_latest.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out))
 

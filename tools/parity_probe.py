@@ -123,7 +123,34 @@ def case_guren():
     return _stats(np.concatenate(eqs))
 
 
-CASES = {"bench": case_bench, "coupled": case_coupled, "heavy": case_heavy, "trace": case_trace,
+def case_hull(steps=30, n=32):
+    """tests/test_gpu_colliders.py's teacher-forced case on the reference's default colliders
+    (primitive_fingertip_collisions=False), the floor under a 1e-7 rad perturbation."""
+    task = dp.TaskConfig(primitive_fingertip_collisions=False)
+    seq = song(dp, "twinkle")
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
+    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
+    lo, hi = dp.model.action_spec(md)
+    rng, prng = np.random.RandomState(5), np.random.RandomState(9)
+    g.reset()
+    tf, fl = [], []
+    for _ in range(steps):
+        a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
+        s = {k: v.cpu().numpy() for k, v in g.get_state().items()}
+        s = {k: s[k] for k in KEYS}
+        o.set_state(s)
+        o2.set_state(perturbed(s, prng))
+        g.step(torch.from_numpy(a).cuda())
+        o.step(a)
+        o2.step(a)
+        qo = o.get_state()["qpos"]
+        tf.append(np.abs(g.get_state()["qpos"].cpu().numpy() - qo).max(axis=1))
+        fl.append(np.abs(o2.get_state()["qpos"] - qo).max(axis=1))
+    return _stats(np.concatenate(tf), np.concatenate(fl))
+
+
+CASES = {"bench": case_bench, "hull": case_hull, "coupled": case_coupled, "heavy": case_heavy, "trace": case_trace,
          "random": case_random, "guren": case_guren}
 
 def diagnose_trace(steps=200, n=8, top=25):

@@ -7,13 +7,12 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT)); sys.path.insert(0, str(ROOT / "tests"))
 dp = importlib.import_module("diffusion-piano_amd")
 lib = importlib.import_module("diffusion-piano_amd._lib")
-from helpers import song
+from helpers import song, tool_hand_kwargs
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 L = lib.load()
 L.ps_debug_timing.argtypes = [C.c_void_p, C.c_void_p]
 NAME = sys.argv[2] if len(sys.argv) > 2 else "crossing_field"
-g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle", **(
-    {"primitive_fingertip_collisions": False} if __import__("os").environ.get("PIANOSIM_HULL") else {})), device="cuda:0")
+g = dp.BatchedPianoEnv(N, song(dp, NAME), dp.TaskConfig(trim_silence=NAME != "twinkle", **tool_hand_kwargs()), device="cuda:0")
 g.reset()
 L.ps_debug_timing(g._h, None)
 gen = torch.Generator(device="cuda:0").manual_seed(1)

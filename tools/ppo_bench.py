@@ -70,7 +70,7 @@ def main():
     env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
                              env_offset=shard.start)
     torch.manual_seed(0)
-    agent = ppo.PPOAgent(env.obs_dim, 45, lr=1e-4, gamma=0.99, epsilon=0.2, batch_size=args.batch,
+    agent = ppo.PPOAgent(env.obs_dim, env.action_dim, lr=1e-4, gamma=0.99, epsilon=0.2, batch_size=args.batch,
                          ppo_epochs=args.epochs, checkpoint_dir="/tmp/ppo_bench_ckpt", use_wandb=False,
                          graphs=not args.eager, sample_seed=1000 + rank, tune_gemms=not args.no_tune,
                          fused=not args.autograd)

@@ -11,16 +11,14 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 dp = importlib.import_module("diffusion-piano_amd")
-from helpers import song  # noqa: E402
+from helpers import song, tool_hand_kwargs  # noqa: E402
 
 
 def throughput(name, n, steps=20):
     import os
     its = os.environ.get("PIANOSIM_NEWTON_ITERS")  # Newton iteration cap (default: the library's)
-    task = dp.TaskConfig(trim_silence=name != "twinkle",
-                         solver_iterations=None if its is None else int(its))
-    if os.environ.get("PIANOSIM_HULL"):  # the box / hull-fingertip hand (reference default colliders)
-        task = dp.TaskConfig(trim_silence=name != "twinkle", primitive_fingertip_collisions=False)
+    task = dp.TaskConfig(trim_silence=name != "twinkle", solver_iterations=None if its is None else int(its),
+                         **tool_hand_kwargs())  # PIANOSIM_HAND: the collider set (bench.py --hand)
     g = dp.BatchedPianoEnv(n, song(dp, name), task, device="cuda:0")
     g.reset()
     gen = torch.Generator(device="cuda:0").manual_seed(12345)
