@@ -24,6 +24,7 @@ struct XShape {
   float er;
   const float* hx;  // hull: the LDS copy of DevModel::hl (x; y at hx + HL_MAX; z at hz; v0 indexes
   const float* hz;  // it), or nullptr: DevModel::hull_v
+  const uint64_t* cells;  // hull: its support cells (DevModel::x_cell), or nullptr: scan all vertices
 };
 
 __device__ __forceinline__ void quat_to_R(float w, float x, float y, float z, float* R) {
@@ -57,6 +58,66 @@ __device__ __forceinline__ f3 nrmz3(f3 a) {
   return n > 0.f ? a * (1.f / n) : a;
 }
 
+// Support cells of a hull (DevModel::x_cell): for each cube-map cell of the direction sphere
+// (face 2 ax + (d_ax < 0), cell (i, j) of the tangent ratios d_(ax+1) / |d_ax|, d_(ax+2) / |d_ax|
+// over [-1, 1], as hull_cell in collide_x.h) the cone over the cell grown by 0.02 in the ratios,
+// spanned by its 4 corner rays c_k. A vertex v is dropped when one vertex u beats it at every
+// corner by more than 1e-5 of the hull's extent: (u - v).c_k > tol for all k holds for every
+// direction in the cone (a non-negative combination of the c_k), and the margin is far above
+// fp32 rounding of the dots, so v never is the fp32 maximum there either. The fp32 scan over
+// the rest returns the first maximal vertex of the full scan.
+inline void hull_support_cells(const double (*v)[3], int n, uint64_t* out) {
+  double ext = 0.0;
+  for (int i = 0; i < n; i++) ext = fmax(ext, sqrt(v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2]));
+  const double tol = 1e-5 * ext, grow = 0.02;
+  for (int face = 0; face < 6; face++)
+    for (int ci = 0; ci < XCG; ci++)
+      for (int cj = 0; cj < XCG; cj++) {
+        const int ax = face / 2;
+        const double sg = face % 2 ? -1.0 : 1.0;
+        double c[4][3];
+        for (int k = 0; k < 4; k++) {
+          const double a = -1.0 + 2.0 * (ci + (k & 1)) / XCG + ((k & 1) ? grow : -grow);
+          const double b = -1.0 + 2.0 * (cj + (k >> 1)) / XCG + ((k >> 1) ? grow : -grow);
+          c[k][ax] = sg;
+          c[k][(ax + 1) % 3] = a;
+          c[k][(ax + 2) % 3] = b;
+        }
+        double P[PS_HULL_MAXVERT][4];
+        for (int i = 0; i < n; i++)
+          for (int k = 0; k < 4; k++) P[i][k] = v[i][0] * c[k][0] + v[i][1] * c[k][1] + v[i][2] * c[k][2];
+        uint64_t mask = 0;
+        for (int i = 0; i < n; i++) {
+          bool dominated = false;
+          for (int u = 0; u < n && !dominated; u++) {
+            if (u == i) continue;
+            bool all = true;
+            for (int k = 0; k < 4 && all; k++) all = P[u][k] - P[i][k] > tol;
+            dominated = all;
+          }
+          if (!dominated) mask |= 1ull << i;
+        }
+        out[(face * XCG + ci) * XCG + cj] = mask;
+      }
+}
+
+// support cell of a (local) direction: the cube-map face of its largest component, the cell of
+// its two tangent ratios over [-1, 1] (hull_support_cells above builds the tables with
+// the same convention; its cells are grown, so rounding at a cell edge picks a cell that still
+// holds the direction). Clamped: any input (NaN included) gives a valid cell.
+__device__ __forceinline__ int hull_cell(f3 d) {
+  const float ex = fabsf(d.x), ey = fabsf(d.y), ez = fabsf(d.z);
+  int ax;
+  float mj, a, b;
+  if (ex >= ey && ex >= ez) { ax = 0; mj = d.x; a = d.y; b = d.z; }
+  else if (ey >= ez) { ax = 1; mj = d.y; a = d.z; b = d.x; }
+  else { ax = 2; mj = d.z; a = d.x; b = d.y; }
+  const float inv = 1.f / fabsf(mj), hg = 0.5f * XCG;
+  const int ia = (int)fminf(fmaxf(fmaf(a, inv, 1.f) * hg, 0.f), XCG - 1.f);
+  const int ib = (int)fminf(fmaxf(fmaf(b, inv, 1.f) * hg, 0.f), XCG - 1.f);
+  return ((2 * ax + (mj < 0.f ? 1 : 0)) * XCG + ia) * XCG + ib;
+}
+
 // support point in direction d (the CPU checker's support(): box corner by sign, 0 on a zero
 // component; capsule end by sign along the axis + radius along d; hull: first maximal vertex)
 __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XShape& s, f3 d) {
@@ -70,6 +131,36 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
   f3 loc;
   if (s.type == PS_GEOM_BOX) {
     loc = mk3(sgn0f(dl.x) * s.hs.x, sgn0f(dl.y) * s.hs.y, sgn0f(dl.z) * s.hs.z);
+  } else if (s.cells) {
+    // the first maximal vertex over the candidates of the direction's support cell (x_cell, its
+    // bits in ascending vertex order, four per trip: their reads issued together) - the same
+    // vertex as the scan over all of them, ~4 candidates instead of ~50 vertices. A zero
+    // direction: every dot is 0, the first vertex.
+    const bool zero = dl.x == 0.f && dl.y == 0.f && dl.z == 0.f;
+    uint64_t msk = zero ? 1ull : s.cells[hull_cell(dl)];
+    float bd = -INFINITY;
+    loc = mk3(0.f, 0.f, 0.f);
+    while (msk) {
+      bool ok[4];
+      f3 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        ok[u] = msk != 0ull;
+        const int id = ok[u] ? __builtin_ctzll(msk) : 0;
+        msk &= msk - 1ull;
+        if (s.hx) {
+          v[u] = mk3(s.hx[s.v0 + id], s.hx[HL_MAX + s.v0 + id], s.hz[s.v0 + id]);
+        } else {
+          const float4 q = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + id]);
+          v[u] = mk3(q.x, q.y, q.z);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const float p = fmaf(dl.z, v[u].z, fmaf(dl.y, v[u].y, dl.x * v[u].x));
+        if (ok[u] && p > bd) { bd = p; loc = v[u]; }
+      }
+    }
   } else if (s.hx) {
     // the first maximal vertex from the LDS copy, four at a time (by coordinate, one 16-byte read
     // per coordinate; a hull starts 4-aligned, its padding repeats the last vertex): the block's
@@ -80,8 +171,8 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
       const float4 X = *reinterpret_cast<const float4*>(s.hx + s.v0 + i0);
       const float4 Y = *reinterpret_cast<const float4*>(s.hx + HL_MAX + s.v0 + i0);
       const float4 Z = *reinterpret_cast<const float4*>(s.hz + s.v0 + i0);
-      float p[4] = {dl.x * X.x + dl.y * Y.x + dl.z * Z.x, dl.x * X.y + dl.y * Y.y + dl.z * Z.y,
-                    dl.x * X.z + dl.y * Y.z + dl.z * Z.z, dl.x * X.w + dl.y * Y.w + dl.z * Z.w};
+      float p[4] = {fmaf(dl.z, Z.x, fmaf(dl.y, Y.x, dl.x * X.x)), fmaf(dl.z, Z.y, fmaf(dl.y, Y.y, dl.x * X.y)),
+                    fmaf(dl.z, Z.z, fmaf(dl.y, Y.z, dl.x * X.z)), fmaf(dl.z, Z.w, fmaf(dl.y, Y.w, dl.x * X.w))};
       f3 v[4] = {mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(X.w, Y.w, Z.w)};
       if (p[1] > p[0]) { p[0] = p[1]; v[0] = v[1]; }
       if (p[3] > p[2]) { p[2] = p[3]; v[2] = v[3]; }
@@ -101,7 +192,7 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         v[j] = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + min(i0 + j, s.nv - 1)]);
-        p[j] = i0 + j < s.nv ? dl.x * v[j].x + dl.y * v[j].y + dl.z * v[j].z : -INFINITY;
+        p[j] = i0 + j < s.nv ? fmaf(dl.z, v[j].z, fmaf(dl.y, v[j].y, dl.x * v[j].x)) : -INFINITY;
       }
 #pragma unroll
       for (int w = 1; w < 8; w *= 2) {

@@ -37,6 +37,10 @@ constexpr int YKEY = 19;
 constexpr int NTRI = MAXDEP * (MAXDEP - 1) / 2;  // (a,b) pairs 1<=a<=b<=8
 constexpr int NKB = 64;        // key-range buckets along y
 constexpr int KGEO = 16;       // floats per key collision record
+// hull support cells: the direction sphere as a cube map of 6 faces x XCG x XCG cells; per hull
+// and cell the vertices that can be the support of a direction in the cell (DevModel::x_cell)
+constexpr int XCG = 4;
+constexpr int XNCELL = 6 * XCG * XCG;
 
 struct DevModel {
   float timestep;
@@ -97,6 +101,11 @@ struct DevModel {
   float x_pos[NXT][3], x_Q[NXT][9], x_hs[NXT][3], x_rb[NXT];
   int x_v0[NXT], x_nv[NXT];    // hull vertices [x_v0, x_v0 + x_nv) of hull_v
   float x_ec[NXT][8];          // hull: an enclosing capsule in the geom frame (p0, p1, radius, pad)
+  // hull: per support cell (hull_cell) the bit mask of the vertices (hull-relative index) that
+  // can be a support of a direction in the cell; the others are beaten by one vertex by a margin
+  // over the whole (grown) cell, so the fp32 scan over the mask finds the same first maximal
+  // vertex as the scan over all of them
+  uint64_t x_cell[NXT][XNCELL];
   int nxpairs;                 // hand-hand pairs with an extra collider: a | b << 8
   int nxpairs_same;            // leading ones within one hand (the rest cross hands)
   int xpair[PS_MAX_XPAIRS];

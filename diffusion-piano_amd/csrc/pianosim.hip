@@ -405,7 +405,10 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
         return fail("hull vertex range out of bounds (4 .. PS_HULL_MAXVERT vertices)");
       if (t == PS_GEOM_BOX && !(d->xgeom_size[h][i][0] > 0 && d->xgeom_size[h][i][1] > 0 && d->xgeom_size[h][i][2] > 0))
         return fail("box half sizes must be positive");
-      if (t == PS_GEOM_HULL) enclosing_capsule(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_ec[e]);
+      if (t == PS_GEOM_HULL) {
+        enclosing_capsule(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_ec[e]);
+        hull_support_cells(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_cell[e]);
+      }
     }
   for (int g = 0; g < NCOLL; g++) {
     m->geom_pathmask[g] = m->body_pathmask[m->geom_body[g]];

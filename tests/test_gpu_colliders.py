@@ -157,14 +157,16 @@ def _rot(rng):
 def test_narrow_phase_matches_checker(dp, ref):
     """The kernel's x_narrow (tools/libxcheck.so launches it one pair per thread) against the
     checker's ref_narrow on random fingertip-scale pairs, inputs rounded to fp32 first:
-    same contact count, depth within 2e-6 m, normal within 1e-3, point within 1e-4 m."""
+    same contact count, depth within 2e-6 m, normal within 1e-3, point within 1e-4 m. The
+    support search over the hulls' support cells (the step kernel's) and over all vertices give
+    bitwise the same results (the cells drop only vertices beaten by a margin over the cell)."""
     import ctypes as C
     from pathlib import Path
 
     from helpers import capsule_points
 
     lib = C.CDLL(str(Path(__file__).resolve().parents[1] / "tools" / "libxcheck.so"))
-    lib.xcheck_run.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    lib.xcheck_run.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     rng = np.random.RandomState(11)
     _, hull = dp.mjcf.convex_hull_collider(capsule_points(0.0085, 0.006))
     hull = hull.astype(np.float32).astype(np.float64)
@@ -211,7 +213,10 @@ def test_narrow_phase_matches_checker(dp, ref):
     dB = torch.from_numpy(np.stack(B)).cuda()
     dv = torch.from_numpy(verts).cuda()
     out = torch.zeros(n, 29, device="cuda:0")
-    assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), out.data_ptr(), n) == 0
+    full = torch.zeros(n, 29, device="cuda:0")
+    assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), full.data_ptr(), n, 0) == 0
+    assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), out.data_ptr(), n, 1) == 0
+    assert torch.equal(out, full), int((out != full).any(dim=1).sum())
     o = out.cpu().numpy()
     bad, hits, counted = [], 0, 0
     for i in range(n):

@@ -3,6 +3,8 @@
 // the CPU checker's ref_narrow (tests/test_gpu_colliders.py). Build: tools/build_xcheck.sh.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "../diffusion-piano_amd/csrc/devmodel.h"
 #include "../diffusion-piano_amd/csrc/prims.h"
 #include "../diffusion-piano_amd/csrc/collide_x.h"
@@ -12,7 +14,7 @@ using namespace ps;
 // packed collider (as ref_narrow): type, centre 3, row-major R 9, p0 3, p1 3, r, half sizes 3,
 // hull first vertex, vertex count (25 floats)
 constexpr int PK = 25;
-__device__ XShape unpack(const float* p) {
+__device__ XShape unpack(const float* p, const uint64_t* cells) {
   XShape s;
   s.type = (int)p[0];
   s.c = ld3(p + 1);
@@ -24,14 +26,16 @@ __device__ XShape unpack(const float* p) {
   s.v0 = (int)p[23];
   s.nv = (int)p[24];
   s.hx = s.hz = nullptr;
+  s.cells = cells && s.type == PS_GEOM_HULL ? cells + (size_t)s.v0 * XNCELL : nullptr;
   if (s.type == 0) s.c = (s.p0 + s.p1) * 0.5f;
   return s;
 }
 
-__global__ void xcheck_kernel(const DevModel* m, const float* a, const float* b, float* out, int n) {
+__global__ void xcheck_kernel(const DevModel* m, const uint64_t* cells, const float* a, const float* b, float* out,
+                              int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const XShape A = unpack(a + PK * i), B = unpack(b + PK * i);
+  const XShape A = unpack(a + PK * i, cells), B = unpack(b + PK * i, cells);
   f3 pos[BB_MAXPT], nrm[BB_MAXPT];
   float dist[BB_MAXPT];
   bool swap;
@@ -47,8 +51,18 @@ __global__ void xcheck_kernel(const DevModel* m, const float* a, const float* b,
 }
 
 extern "C" {
-// hull vertices [nv][4] (device), pairs a/b [n][25] (device), out [n][29] (device)
-int xcheck_run(const float* hull_v, int nv, const float* a, const float* b, float* out, int n) {
+// host only (CPU tests): the support cells of one hull, vertices [n][3] -> out [XNCELL]
+int xcheck_cells(const double* v, int n, uint64_t* out) {
+  if (n < 1 || n > PS_HULL_MAXVERT) return -1;
+  hull_support_cells(reinterpret_cast<const double(*)[3]>(v), n, out);
+  return XNCELL;
+}
+int xcheck_cell_grid(void) { return XCG; }
+
+// hull vertices [nv][4] (device), pairs a/b [n][25] (device), out [n][29] (device); cells != 0:
+// the support search over the hulls' support cells (the step kernel's, DevModel::x_cell, built
+// for every hull (v0, nv) the pairs name), else over all vertices
+int xcheck_run(const float* hull_v, int nv, const float* a, const float* b, float* out, int n, int cells) {
   if (nv > NH * PS_HAND_HULLVERT) return -1;
   DevModel* hm = new DevModel();
   DevModel* dm = nullptr;
@@ -56,9 +70,33 @@ int xcheck_run(const float* hull_v, int nv, const float* a, const float* b, floa
   if (hipMemcpy(dm, hm, sizeof(DevModel), hipMemcpyHostToDevice) != hipSuccess) return -3;
   delete hm;
   if (nv && hipMemcpy(dm->hull_v, hull_v, sizeof(float) * 4 * nv, hipMemcpyDeviceToDevice) != hipSuccess) return -4;
-  hipLaunchKernelGGL(xcheck_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dm, a, b, out, n);
+  uint64_t* dcells = nullptr;
+  if (cells && nv) {
+    std::vector<float> hv((size_t)4 * nv), ha((size_t)PK * n), hb((size_t)PK * n);
+    if (hipMemcpy(hv.data(), hull_v, sizeof(float) * 4 * nv, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ha.data(), a, sizeof(float) * PK * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hb.data(), b, sizeof(float) * PK * n, hipMemcpyDeviceToHost) != hipSuccess)
+      return -6;
+    std::vector<uint64_t> hc((size_t)nv * XNCELL, 0ull);
+    std::vector<char> done(nv, 0);
+    for (const std::vector<float>* src : {&ha, &hb})
+      for (int i = 0; i < n; i++) {
+        const float* p = src->data() + (size_t)PK * i;
+        const int v0 = (int)p[23], cnt = (int)p[24];
+        if ((int)p[0] != PS_GEOM_HULL || v0 < 0 || cnt < 1 || cnt > PS_HULL_MAXVERT || v0 + cnt > nv || done[v0]) continue;
+        done[v0] = 1;
+        std::vector<double> vd((size_t)3 * cnt);
+        for (int k = 0; k < cnt; k++)
+          for (int c = 0; c < 3; c++) vd[3 * k + c] = hv[4 * (size_t)(v0 + k) + c];
+        hull_support_cells(reinterpret_cast<const double(*)[3]>(vd.data()), cnt, hc.data() + (size_t)v0 * XNCELL);
+      }
+    if (hipMalloc(&dcells, sizeof(uint64_t) * hc.size()) != hipSuccess) return -7;
+    if (hipMemcpy(dcells, hc.data(), sizeof(uint64_t) * hc.size(), hipMemcpyHostToDevice) != hipSuccess) return -8;
+  }
+  hipLaunchKernelGGL(xcheck_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dm, dcells, a, b, out, n);
   if (hipDeviceSynchronize() != hipSuccess) return -5;
   hipFree(dm);
+  if (dcells) hipFree(dcells);
   return 0;
 }
 }
