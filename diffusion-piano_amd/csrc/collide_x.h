@@ -27,6 +27,16 @@ struct XShape {
   const uint64_t* cells;  // hull: its support cells (DevModel::x_cell), or nullptr: scan all vertices
 };
 
+// a collider moved by -o (its centre, segment and enclosing capsule; rotations, half sizes and
+// hull vertices are frame-relative)
+__device__ __forceinline__ void x_shift(XShape& s, f3 o) {
+  s.c = s.c - o;
+  s.p0 = s.p0 - o;
+  s.p1 = s.p1 - o;
+  s.e0 = s.e0 - o;
+  s.e1 = s.e1 - o;
+}
+
 __device__ __forceinline__ void quat_to_R(float w, float x, float y, float z, float* R) {
   const float n = rsqrtf(w * w + x * x + y * y + z * z);
   w *= n; x *= n; y *= n; z *= n;
@@ -596,6 +606,22 @@ __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XS
   pos[0] = p;
   nrm[0] = n;
   dist[0] = -depth;
+  return cnt;
+}
+
+// x_narrow in a frame at geom2's centre (the step kernel's narrow phase): the support points and
+// portal arithmetic at the pair's scale (centimetres) instead of world coordinates (~0.5 m: an
+// fp32 ulp of 6e-8 m on every support point, against MPR's 1e-6 m tolerance, steers the portal
+// differently from the fp64 checker's); the contact points back in world coordinates
+__device__ __forceinline__ int x_narrow_local(const DevModel* __restrict__ m, XShape A, XShape B, f3 (&pos)[BB_MAXPT],
+                                              float (&dist)[BB_MAXPT], f3 (&nrm)[BB_MAXPT], bool& swap,
+                                              int* its = nullptr) {
+  const f3 org = B.c;
+  x_shift(A, org);
+  x_shift(B, org);
+  const int cnt = x_narrow(m, A, B, pos, dist, nrm, swap, its);
+#pragma unroll
+  for (int j = 0; j < BB_MAXPT; j++) pos[j] = pos[j] + org;
   return cnt;
 }
 

@@ -178,33 +178,40 @@ def test_narrow_phase_matches_checker(dp, ref):
     A, B, ra, rb = [], [], [], []
     for i in range(6000):
         kind = i % 5
+        # where the hands are: every pair at a world position 0.1 - 0.7 m from the origin (the
+        # narrow phase runs in a frame at geom2's centre; fp32 world coordinates would not do)
+        w = rng.uniform([-0.6, -0.6, 0.0], [0.6, 0.6, 0.3]).astype(np.float32)
         c2 = (rng.normal(size=3) * 0.012).astype(np.float32)
         Ra, Rb = _rot(rng), _rot(rng)
         if kind == 0:    # key-size box vs fingertip hull
             hs = np.array([0.0117, 0.0235, 0.0113], np.float32)
-            a, r1 = _pack("box", R=Ra, hs=hs), ref.shape("box", R=Ra, hs=hs)
+            a, r1 = _pack("box", c=w, R=Ra, hs=hs), ref.shape("box", c=w, R=Ra, hs=hs)
             v0, nv, vv = hv["tip"]
-            c2 = (c2 * 2).astype(np.float32)
+            c2 = (c2 * 2 + w).astype(np.float32)
             b, r2 = _pack("hull", c=c2, R=Rb, v0=v0, nv=nv), ref.shape("hull", c=c2, R=Rb, verts=vv)
         elif kind == 1:  # hull vs hull
             v0, nv, vv = hv["tip"]
-            a, r1 = _pack("hull", R=Ra, v0=v0, nv=nv), ref.shape("hull", R=Ra, verts=vv)
+            c2 = (c2 + w).astype(np.float32)
+            a, r1 = _pack("hull", c=w, R=Ra, v0=v0, nv=nv), ref.shape("hull", c=w, R=Ra, verts=vv)
             b, r2 = _pack("hull", c=c2, R=Rb, v0=v0, nv=nv), ref.shape("hull", c=c2, R=Rb, verts=vv)
         elif kind == 2:  # capsule vs hull (cube)
             d = Ra[:, 2] * 0.01
-            p0, p1 = (-d).astype(np.float32), d.astype(np.float32)
+            p0, p1 = (w - d).astype(np.float32), (w + d).astype(np.float32)
+            c2 = (c2 + w).astype(np.float32)
             a, r1 = _pack("capsule", p0=p0, p1=p1, r=0.008), ref.shape("capsule", p0=p0, p1=p1, r=np.float32(0.008))
             v0, nv, vv = hv["cube"]
             b, r2 = _pack("hull", c=c2, R=Rb, v0=v0, nv=nv), ref.shape("hull", c=c2, R=Rb, verts=vv)
         elif kind == 3:  # box vs box
             h1 = rng.uniform(0.005, 0.015, 3).astype(np.float32)
             h2 = rng.uniform(0.005, 0.015, 3).astype(np.float32)
-            a, r1 = _pack("box", R=Ra, hs=h1), ref.shape("box", R=Ra, hs=h1)
+            c2 = (c2 + w).astype(np.float32)
+            a, r1 = _pack("box", c=w, R=Ra, hs=h1), ref.shape("box", c=w, R=Ra, hs=h1)
             b, r2 = _pack("box", c=c2, R=Rb, hs=h2), ref.shape("box", c=c2, R=Rb, hs=h2)
         else:            # capsule vs box
             d = Ra[:, 2] * 0.01
-            p0, p1 = (-d).astype(np.float32), d.astype(np.float32)
+            p0, p1 = (w - d).astype(np.float32), (w + d).astype(np.float32)
             h2 = rng.uniform(0.005, 0.015, 3).astype(np.float32)
+            c2 = (c2 + w).astype(np.float32)
             a, r1 = _pack("capsule", p0=p0, p1=p1, r=0.008), ref.shape("capsule", p0=p0, p1=p1, r=np.float32(0.008))
             b, r2 = _pack("box", c=c2, R=Rb, hs=h2), ref.shape("box", c=c2, R=Rb, hs=h2)
         A.append(a); B.append(b); ra.append(r1); rb.append(r2)

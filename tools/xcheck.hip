@@ -26,8 +26,10 @@ __device__ XShape unpack(const float* p, const uint64_t* cells) {
   s.v0 = (int)p[23];
   s.nv = (int)p[24];
   s.hx = s.hz = nullptr;
+  s.er = 0.f;
   s.cells = cells && s.type == PS_GEOM_HULL ? cells + (size_t)s.v0 * XNCELL : nullptr;
   if (s.type == 0) s.c = (s.p0 + s.p1) * 0.5f;
+  s.e0 = s.e1 = s.c;
   return s;
 }
 
@@ -39,7 +41,7 @@ __global__ void xcheck_kernel(const DevModel* m, const uint64_t* cells, const fl
   f3 pos[BB_MAXPT], nrm[BB_MAXPT];
   float dist[BB_MAXPT];
   bool swap;
-  const int cnt = x_narrow(m, A, B, pos, dist, nrm, swap);
+  const int cnt = x_narrow_local(m, A, B, pos, dist, nrm, swap);  // the step kernel's narrow phase
   float* o = out + i * (1 + 7 * BB_MAXPT);
   o[0] = (float)cnt;
   for (int j = 0; j < BB_MAXPT; j++) {
