@@ -94,3 +94,23 @@ def assert_parity(e, floor, what="", tol=1e-4, well=1e-5, p99_ceil=PARITY_P99_CE
     assert np.percentile(e, 99) <= min(max(tol, 2.0 * np.percentile(floor, 99)), p99_ceil), msg
     assert e.max() <= max_ceil, msg
     return msg
+
+
+def assert_flip_rates(e, floor, what="", ts=(1e-3, 1e-2), p99_cap=0.1, slack=0.01):
+    """The whole-step gate of the box / hull hand, whose MPR contact normals are piecewise
+    constant over the hulls' faces (a portal near a face edge switches faces under any tiny
+    change of its input, in the fp64 checker too): median < 1e-5; for each threshold t the
+    fraction of env-steps the GPU moves by more than t at most 1.5x the fraction the checker
+    moves itself under a 1e-7 rad perturbation (`floor`) + `slack`; p99 within 2x the floor's p99
+    and below `p99_cap`."""
+    e, floor = np.asarray(e, np.float64), np.asarray(floor, np.float64)
+    rates = {t: (float(np.mean(e > t)), float(np.mean(floor > t))) for t in ts}
+    msg = (f"{what}: n {e.size}, median {np.median(e):.2e}, p99 {np.percentile(e, 99):.2e}, max {e.max():.2e}; "
+           f"floor median {np.median(floor):.2e} p99 {np.percentile(floor, 99):.2e}; flip rates (gpu, floor) " +
+           ", ".join(f">{t:.0e}: {a:.3f} {b:.3f}" for t, (a, b) in rates.items()))
+    print(msg)
+    assert np.median(e) < 1e-5, msg
+    for t, (a, b) in rates.items():
+        assert a <= 1.5 * b + slack, msg
+    assert np.percentile(e, 99) <= min(2.0 * np.percentile(floor, 99), p99_cap), msg
+    return msg

@@ -4,13 +4,19 @@ csrc/collide_x.h) against the CPU checker on a hand whose palm and little-finger
 are boxes and whose fingertips are convex hulls (helpers.box_hull_hand), loaded through the
 MJCF path (mesh assets with inline vertices).
 
-Tolerances: fp32 kernel vs fp64 checker, one control step from the same state, as the capsule
-hand's parity tests (tests/test_gpu_parity.py): qpos median < 1e-5, p99 < 5e-4.
+Tolerances: fp32 kernel vs fp64 checker from the same state. MPR's contact normal is piecewise
+constant over the hulls' faces (as in MuJoCo's libccd path), so a portal that ends near a face
+edge switches faces under any tiny change of its input: the checker itself, stepped from the
+state with the hand joints moved by 1e-7 rad, moves by more than 1e-3 on ~8% of the env-steps
+(the capsule hand: ~0.1%). The whole-step gates are therefore the flip-rate comparison
+(helpers.assert_flip_rates: median < 1e-5; the fraction of env-steps moved by more than 1e-3 /
+1e-2 at most 1.5x the checker's own + 1%; p99 at most 2x the checker's own and below 0.1), and
+the narrow phase itself is held pair by pair (test_narrow_phase_matches_checker).
 """
 import numpy as np
 import pytest
 
-from helpers import box_hull_hand, song
+from helpers import assert_flip_rates, box_hull_hand, perturbed, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -33,12 +39,8 @@ def task(dp, request):
 
 def test_box_hull_hand_teacher_forced(dp, ref, task):
     """GPU vs checker, one control step from the same state, against the model's own fp64
-    sensitivity: the checker stepped from the same state with the hand joints moved by 1e-6
-    rad (the scale of MPR's 1e-6 tolerance, at which the fp32 and fp64 portals stop). MPR's
-    normal is piecewise constant over the hulls' faces (as in MuJoCo), so a tolerance-level
-    difference can switch a contact to the next face; the box/hull hand's p99 one-step
-    sensitivity is ~30x the capsule hand's (fp64 against fp64). The GPU must stay at that
-    floor: median < 1e-5, qpos p99 within 2x the floor's, reward p95 within 2x the floor's."""
+    sensitivity (the checker stepped from the state with the hand joints moved by 1e-7 rad):
+    helpers.assert_flip_rates on qpos; reward p95 within 2x the checker's own."""
     n = 32
     seq = song(dp, "twinkle")
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
@@ -54,9 +56,7 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
         a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
         s = {k: v for k, v in _gs(g).items() if k in KEYS}
         o.set_state(s)
-        s2 = dict(s)
-        s2["qpos"] = s["qpos"].astype(np.float64) + np.concatenate([np.zeros((n, 88)), prng.normal(0, 1e-6, (n, 52))], 1)
-        o2.set_state(s2)
+        o2.set_state(perturbed(s, prng))
         _, rg, _, _ = g.step(torch.from_numpy(a).cuda())
         _, ro, _, _ = o.step(a)
         _, ro2, _, _ = o2.step(a)
@@ -71,10 +71,7 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
             for kind, key, g1, g2, dist in o.contacts(i):
                 kinds.add((kind, g1 >= 40, g2 >= 40))
     e, f = np.concatenate(errs), np.concatenate(floor)
-    print(f"box/hull hand: qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}; "
-          f"1e-6 rad floor median {np.median(f):.2e} p99 {np.percentile(f, 99):.2e}")
-    assert np.median(e) < 1e-5, (np.median(e), np.median(f))
-    assert np.percentile(e, 99) <= max(5e-4, 2 * np.percentile(f, 99)), (np.percentile(e, 99), np.percentile(f, 99))
+    assert_flip_rates(e, f, "box/hull hand, control step")
     re, rf = np.concatenate(rerr), np.concatenate(rfloor)
     assert np.percentile(re, 95) <= max(1e-3, 2 * np.percentile(rf, 95)), (np.percentile(re, 95), np.percentile(rf, 95))
     same = np.mean(np.concatenate(ncg) == np.concatenate(nco))
@@ -87,7 +84,9 @@ def test_box_hull_hand_one_substep(dp, ref):
     """The reference's default colliders (palm boxes, hull fingertips) at the one-substep gate:
     GPU vs checker for ONE physics substep from the same states (rollout states of the GPU under
     random actions), where the contact set and the MPR portals come from the same positions and
-    nothing compounds: qpos median < 1e-6, p99 < 5e-5, qvel (qacc h) relative p99 < 1e-3."""
+    nothing compounds: qpos median < 1e-6, qacc relative median < 1e-4; a face switch of an MPR
+    normal is a step change even here, so the tail is held by flip rates against the checker's own
+    (1e-7 rad) at 1e-5 and 1e-4, p99 below 1e-2."""
     n = 64
     seq = song(dp, "twinkle")
     task1 = dp.TaskConfig(primitive_fingertip_collisions=False, control_timestep=0.005)
@@ -96,33 +95,37 @@ def test_box_hull_hand_one_substep(dp, ref):
     assert md.n_substeps == 1
     roll = dp.BatchedPianoEnv(n, seq, task10, device="cuda:0", canonical_actions=False)
     g = dp.BatchedPianoEnv(n, seq, task1, device="cuda:0", canonical_actions=False)
-    o = ref.OracleEnv(md, st, tc, n)
+    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
     lo, hi = dp.model.action_spec(md)
-    rng = np.random.RandomState(6)
+    rng, prng = np.random.RandomState(6), np.random.RandomState(7)
     roll.reset()
-    eq, ea, ncon = [], [], 0
+    eq, ea, fq, ncon = [], [], [], 0
     for t in range(12):
         roll.step(torch.from_numpy(rng.uniform(lo, hi, (n, 45)).astype(np.float32)).cuda())
         s = {k: v for k, v in _gs(roll).items() if k in KEYS}
         a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
         g.set_state(s)
         o.set_state(s)
+        o2.set_state(perturbed(s, prng))
         g.step(torch.from_numpy(a).cuda())
         o.step(a)
+        o2.step(a)
         sg, so = _gs(g), o.get_state()
         eq.append(np.abs(sg["qpos"] - so["qpos"]).max(axis=1))
+        fq.append(np.abs(o2.get_state()["qpos"] - so["qpos"]).max(axis=1))
         v0 = s["qvel"].astype(np.float64)
         acc_o, acc_g = (so["qvel"] - v0) / 0.005, (sg["qvel"] - v0) / 0.005
         ea.append(np.abs(acc_g - acc_o).max(axis=1) / np.maximum(np.abs(acc_o).max(axis=1), 1.0))
         ncon += int(o.contact_count().sum())
-    eq, ea = np.concatenate(eq), np.concatenate(ea)
+    eq, ea, fq = np.concatenate(eq), np.concatenate(ea), np.concatenate(fq)
     msg = (f"box/hull hand, one substep: {ncon} contacts; qpos err median {np.median(eq):.2e} p99 "
            f"{np.percentile(eq, 99):.2e} max {eq.max():.2e}; qacc rel err median {np.median(ea):.2e} p99 "
            f"{np.percentile(ea, 99):.2e} max {ea.max():.2e}")
     print(msg)
     assert ncon > 0
-    assert np.median(eq) < 1e-6 and np.percentile(eq, 99) < 5e-5, msg
-    assert np.percentile(ea, 99) < 1e-3, msg
+    # the substep gate of the capsule hand where no face switched (median), flip rates elsewhere
+    assert np.median(eq) < 1e-6 and np.median(ea) < 1e-4, msg
+    assert_flip_rates(eq, fq, "box/hull hand, one substep", ts=(1e-5, 1e-4), p99_cap=1e-2)
 
 
 def test_box_hull_hand_duplicates_bitwise(dp, task):

@@ -38,7 +38,10 @@ def _stats(e, floor=None):
     if floor is not None:
         calm = np.asarray(floor) < 1e-5
         out.update(p99_well=float(np.percentile(e[calm], 99)) if calm.any() else None, n_well=int(calm.sum()),
-                   floor_p99=float(np.percentile(floor, 99)))
+                   floor_p99=float(np.percentile(floor, 99)), floor_median=float(np.median(floor)))
+        f = np.asarray(floor)
+        for t in (1e-4, 1e-3, 1e-2):  # flip rates: env-steps moved by more than t, GPU vs the checker's own
+            out[f"frac_gt_{t:.0e}"] = [float(np.mean(e > t)), float(np.mean(f > t))]
     return out
 
 
