@@ -21,7 +21,7 @@ for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
     stats.append(g.solver_stats().cpu().numpy())
 st = np.stack(stats)  # [10, N, 4]
-NPH = 40
+NPH = 48
 out = np.zeros((N, NPH), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
 names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest",
@@ -45,6 +45,12 @@ m = out[:, 28:32].astype(np.float64).sum(axis=0)  # box / hull narrow-phase roun
 if m[1] > 0 or m[3] > 0:
     print(f"box/hull narrow phase: piano {m[1] / N / 100:.2f} rounds/substep, {m[0] / max(m[1], 1):.1f} MPR steps of the "
           f"slowest lane per round; hand-hand {m[3] / N / 100:.2f} rounds/substep, {m[2] / max(m[3], 1):.1f} steps")
+h = out[:, 38:46].astype(np.float64).sum(axis=0)
+if h[0] > 0:
+    print(f"hand-hand pairs per substep: {h[7] / N / 100:.2f} past the spheres, {h[0] / N / 100:.2f} past the enclosing "
+          f"capsules (substeps with any: {h[4] / N / 100:.3f}), {h[1] / N / 100:.3f} with a contact; MPR steps per pair "
+          f"{h[2] / max(h[0], 1):.2f} (contact pairs {h[3] / max(h[1], 1):.2f}, others {(h[2] - h[3]) / max(h[0] - h[1], 1):.2f}); "
+          f"piano hull pairs per substep {h[5] / N / 100:.2f}, {h[6] / N / 100:.3f} with a contact")
 if c[1] > 0 and c[4] > 0:
     print(f"Newton by substep: first {c[0] / c[1]:.2f} iterations, later {c[2] / c[4]:.2f} "
           f"(guessed piece held in {100 * c[3] / c[4]:.1f}% of the later substeps)")

@@ -26,7 +26,7 @@ names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB level
          12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
          8: "nt:J'f", 6: "integrate", 5: "final+task"}  # the slots of phase_timing.py (Newton solve)
 idx = list(names)
-out = np.zeros((N, 40), np.uint64)
+out = np.zeros((N, 48), np.uint64)
 means, maxes, worst_rows, mean_rows, ms, piv = [], [], [], [], [], []
 for s in range(STEPS):
     a = torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1
