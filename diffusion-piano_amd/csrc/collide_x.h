@@ -225,52 +225,10 @@ struct MprPt {
   f3 v, a, b;
 };
 __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < MPR_EPSF; }
-// a hull vertex (hull-relative index id) from the LDS copy or DevModel::hull_v
-__device__ __forceinline__ f3 hull_vertex(const DevModel* __restrict__ m, const XShape& s, int id) {
-  if (s.hx) return mk3(s.hx[s.v0 + id], s.hx[HL_MAX + s.v0 + id], s.hz[s.v0 + id]);
-  const float4 q = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + id]);
-  return mk3(q.x, q.y, q.z);
-}
-
-// The supports of A along d and of B along -d. When both are hulls with support cells (the
-// hand-hand fingertip pairs), their cell masks and candidate vertices are read in one interleaved
-// loop - the two searches' memory latencies overlap instead of adding up; each search is the
-// x_support one (ascending candidates, the same dots and strict compares: the same vertices).
 __device__ __forceinline__ MprPt mpr_sup(const DevModel* __restrict__ m, const XShape& A, const XShape& B, f3 d) {
   MprPt p;
-  if (A.type == PS_GEOM_HULL && A.cells && B.type == PS_GEOM_HULL && B.cells) {
-    const f3 da = mtv3(A.R, d), db = mtv3(B.R, d * -1.f);
-    uint64_t ma = (da.x == 0.f && da.y == 0.f && da.z == 0.f) ? 1ull : A.cells[hull_cell(da)];
-    uint64_t mb = (db.x == 0.f && db.y == 0.f && db.z == 0.f) ? 1ull : B.cells[hull_cell(db)];
-    float ba = -INFINITY, bb = -INFINITY;
-    f3 la = mk3(0.f, 0.f, 0.f), lb = la;
-    while (ma | mb) {
-      bool oa[4], ob[4];
-      f3 va[4], vb[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        oa[u] = ma != 0ull;
-        ob[u] = mb != 0ull;
-        const int ia = oa[u] ? __builtin_ctzll(ma) : 0, ib = ob[u] ? __builtin_ctzll(mb) : 0;
-        ma &= ma - 1ull;
-        mb &= mb - 1ull;
-        va[u] = hull_vertex(m, A, ia);
-        vb[u] = hull_vertex(m, B, ib);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const float pa = fmaf(da.z, va[u].z, fmaf(da.y, va[u].y, da.x * va[u].x));
-        const float pb = fmaf(db.z, vb[u].z, fmaf(db.y, vb[u].y, db.x * vb[u].x));
-        if (oa[u] && pa > ba) { ba = pa; la = va[u]; }
-        if (ob[u] && pb > bb) { bb = pb; lb = vb[u]; }
-      }
-    }
-    p.a = A.c + mv3(A.R, la);
-    p.b = B.c + mv3(B.R, lb);
-  } else {
-    p.a = x_support(m, A, d);
-    p.b = x_support(m, B, d * -1.f);
-  }
+  p.a = x_support(m, A, d);
+  p.b = x_support(m, B, d * -1.f);
   p.v = p.a - p.b;
   return p;
 }
