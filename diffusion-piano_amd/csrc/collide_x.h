@@ -22,8 +22,6 @@ struct XShape {
   int v0, nv;      // hull vertices in DevModel::hull_v (geom frame)
   f3 e0, e1;       // hull: an enclosing capsule (world), radius er
   float er;
-  const float* hx;  // hull: the LDS copy of DevModel::hl (x; y at hx + HL_MAX; z at hz; v0 indexes
-  const float* hz;  // it), or nullptr: DevModel::hull_v
   const uint64_t* cells;  // hull: its support cells (DevModel::x_cell), or nullptr: scan all vertices
 };
 
@@ -158,36 +156,14 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
         ok[u] = msk != 0ull;
         const int id = ok[u] ? __builtin_ctzll(msk) : 0;
         msk &= msk - 1ull;
-        if (s.hx) {
-          v[u] = mk3(s.hx[s.v0 + id], s.hx[HL_MAX + s.v0 + id], s.hz[s.v0 + id]);
-        } else {
-          const float4 q = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + id]);
-          v[u] = mk3(q.x, q.y, q.z);
-        }
+        const float4 q = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + id]);
+        v[u] = mk3(q.x, q.y, q.z);
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         const float p = fmaf(dl.z, v[u].z, fmaf(dl.y, v[u].y, dl.x * v[u].x));
         if (ok[u] && p > bd) { bd = p; loc = v[u]; }
       }
-    }
-  } else if (s.hx) {
-    // the first maximal vertex from the LDS copy, four at a time (by coordinate, one 16-byte read
-    // per coordinate; a hull starts 4-aligned, its padding repeats the last vertex): the block's
-    // best by a 2-level tree (ties to the lower index), then against the running best
-    float bd = -INFINITY;
-    loc = mk3(0.f, 0.f, 0.f);
-    for (int i0 = 0; i0 < s.nv; i0 += 4) {
-      const float4 X = *reinterpret_cast<const float4*>(s.hx + s.v0 + i0);
-      const float4 Y = *reinterpret_cast<const float4*>(s.hx + HL_MAX + s.v0 + i0);
-      const float4 Z = *reinterpret_cast<const float4*>(s.hz + s.v0 + i0);
-      float p[4] = {fmaf(dl.z, Z.x, fmaf(dl.y, Y.x, dl.x * X.x)), fmaf(dl.z, Z.y, fmaf(dl.y, Y.y, dl.x * X.y)),
-                    fmaf(dl.z, Z.z, fmaf(dl.y, Y.z, dl.x * X.z)), fmaf(dl.z, Z.w, fmaf(dl.y, Y.w, dl.x * X.w))};
-      f3 v[4] = {mk3(X.x, Y.x, Z.x), mk3(X.y, Y.y, Z.y), mk3(X.z, Y.z, Z.z), mk3(X.w, Y.w, Z.w)};
-      if (p[1] > p[0]) { p[0] = p[1]; v[0] = v[1]; }
-      if (p[3] > p[2]) { p[2] = p[3]; v[2] = v[3]; }
-      if (p[2] > p[0]) { p[0] = p[2]; v[0] = v[2]; }
-      if (p[0] > bd) { bd = p[0]; loc = v[0]; }
     }
   } else {
     // the first maximal vertex, eight at a time: the block's loads issued together, its best by

@@ -21,7 +21,6 @@ constexpr int NDT = NH * ND;   // 52 hand dofs (lane l <-> hand dof l)
 constexpr int NGT = NH * NG;   // 40 capsules
 constexpr int NX = PS_HAND_NXGEOM;
 constexpr int NXT = NH * NX;   // 24 box / hull colliders: lanes NGT .. NGT + NXT - 1
-constexpr int HL_MAX = 640;   // hull vertices (padded to 4 per hull) the LDS copy holds
 constexpr int NCOLL = NGT + NXT;  // global collider ids: capsules, then the extra colliders
 static_assert(NCOLL <= 64, "one lane per collider");
 constexpr int NTT = NH * PS_HAND_NTENDON;
@@ -110,11 +109,6 @@ struct DevModel {
   int nxpairs_same;            // leading ones within one hand (the rest cross hands)
   int xpair[PS_MAX_XPAIRS];
   alignas(16) float hull_v[NH * PS_HAND_HULLVERT][4];  // geom frame (w unused)
-  // the same vertices by coordinate for the LDS copy of the hand-hand narrow phase (collide2):
-  // hull e's at [x_lv0[e], + x_nv[e] rounded up to 4); hl_n = 0: no copy (global hull_v)
-  alignas(16) float hl[3][HL_MAX];
-  int hl_n;
-  int x_lv0[NXT];
   // triangular (a,b) table for the LDL update
   int tri_a[NTRI + 8], tri_b[NTRI + 8];
   // v2 lane-owned topology (packed, loaded into registers once per launch)

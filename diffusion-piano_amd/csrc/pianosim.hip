@@ -419,20 +419,6 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       for (int k = 0; k < 3; k++) m->hull_v[h * PS_HAND_HULLVERT + v][k] = (float)d->hull_vert[h][v][k];
       m->hull_v[h * PS_HAND_HULLVERT + v][3] = 0.f;
     }
-  // the hull vertices compacted by coordinate (DevModel::hl), each hull padded to a multiple of 4
-  // by repeats of its last vertex (never a first maximum); none when they exceed HL_MAX
-  m->hl_n = 0;
-  for (int e = 0; e < NXT; e++) {
-    m->x_lv0[e] = 0;
-    if (m->x_type[e] != PS_GEOM_HULL) continue;
-    const int nv4 = (m->x_nv[e] + 3) & ~3;
-    if (m->hl_n + nv4 > HL_MAX) { m->hl_n = -1; break; }
-    m->x_lv0[e] = m->hl_n;
-    for (int j = 0; j < nv4; j++)
-      for (int k = 0; k < 3; k++) m->hl[k][m->hl_n + j] = m->hull_v[m->x_v0[e] + std::min(j, m->x_nv[e] - 1)][k];
-    m->hl_n += nv4;
-  }
-  if (m->hl_n < 0) m->hl_n = 0;
   if (d->n_xpairs < 0 || d->n_xpairs > PS_MAX_XPAIRS) return fail("bad n_xpairs");
   m->nxpairs = d->n_xpairs;
   for (int i = 0; i < d->n_xpairs; i++) {

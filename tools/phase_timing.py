@@ -21,12 +21,13 @@ for i in range(10):
     g.step(torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1)
     stats.append(g.solver_stats().cpu().numpy())
 st = np.stack(stats)  # [10, N, 4]
-NPH = 48
+NPH = 56
 out = np.zeros((N, NPH), np.uint64)
 L.ps_debug_timing(g._h, out.ctypes.data)
 names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest",
          11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs", 18: "newton:prep", 3: "factor", 4: "solve_smooth",
-         12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
+         46: "nt:setup-keys", 47: "nt:setup-park", 48: "nt:setup-dofrows", 49: "nt:setup-keyrows",
+         50: "nt:setup-contacts", 12: "nt:setup-rest", 51: "nt:rows", 13: "nt:grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
          8: "nt:J'f", 6: "integrate", 5: "final+task", 32: "xpiano:cand", 33: "xpiano:refine", 34: "xpiano:narrow",
          35: "xpairs:sphere", 36: "xpairs:refine", 37: "xpairs:narrow"}
 tot = out[:, [i for i in names]].astype(np.float64).sum(axis=1)

@@ -23,10 +23,11 @@ for _ in range(3):
 L.ps_debug_timing(g._h, None)
 names = {24: "kin:prologue", 25: "kin:levels", 0: "kin:rest", 26: "dyn:CRB levels", 27: "dyn:M rows", 1: "dyn:rest",
          11: "coll:piano cnt", 7: "coll:piano wr", 2: "coll:pairs", 18: "newton:prep", 3: "factor", 4: "solve_smooth",
-         12: "nt:setup", 13: "nt:rows+grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
+         46: "nt:setup-keys", 47: "nt:setup-park", 48: "nt:setup-dofrows", 49: "nt:setup-keyrows",
+         50: "nt:setup-contacts", 12: "nt:setup-rest", 51: "nt:rows", 13: "nt:grad", 14: "nt:hessian", 15: "nt:factor", 16: "nt:solve", 17: "nt:linesearch",
          8: "nt:J'f", 6: "integrate", 5: "final+task"}  # the slots of phase_timing.py (Newton solve)
 idx = list(names)
-out = np.zeros((N, 48), np.uint64)
+out = np.zeros((N, 56), np.uint64)
 means, maxes, worst_rows, mean_rows, ms, piv = [], [], [], [], [], []
 for s in range(STEPS):
     a = torch.rand(N, 45, device="cuda:0", generator=gen) * 2 - 1

@@ -25,7 +25,6 @@ __device__ XShape unpack(const float* p, const uint64_t* cells) {
   s.hs = ld3(p + 20);
   s.v0 = (int)p[23];
   s.nv = (int)p[24];
-  s.hx = s.hz = nullptr;
   s.er = 0.f;
   s.cells = cells && s.type == PS_GEOM_HULL ? cells + (size_t)s.v0 * XNCELL : nullptr;
   if (s.type == 0) s.c = (s.p0 + s.p1) * 0.5f;
