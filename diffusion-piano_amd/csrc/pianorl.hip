@@ -531,6 +531,7 @@ __global__ void colsums_final_kernel(ColSums cs, int nchunks) {
 }
 
 #include "mlp_step.inc"
+#include "mlp_split.inc"
 
 }  // namespace
 
@@ -717,6 +718,16 @@ int prl_colsums(int n, const float* const* src, const int* cols, const float* sc
 
 // ---------------------------------------------------------------- fused minibatch step on the matrix cores (mlp_step.inc)
 namespace {
+// the column-split rows kernel's shape conditions: <= 256 rows, state width <= 384, hidden
+// widths 128 or 256 (mlp_split.inc)
+bool split_shapes(const prl_net* nets, int sdim, int B) {
+  if (B > mlp::SPLIT_MAX_ROWS || sdim > mlp::SPLIT_MAX_SDIM) return false;
+  for (int i = 0; i < 2; i++)
+    for (int l = 0; l + 1 < nets[i].nlayers; l++)
+      if (nets[i].layer[l].out != 128 && nets[i].layer[l].out != 256) return false;
+  return true;
+}
+
 // work layout of prl_mlp_step: the per-tile partial rows [tiles][total] (bias / LayerNorm /
 // log_std column sums and the 6 logged sums), then per network the inputs of layers 1..3
 // [B][in] and every layer's dZ [B][out]; the reduction entries and the weight-gradient tiles
@@ -786,6 +797,21 @@ int mlp_layout(const prl_net* nets, int sdim, int B, float* work, float* log_row
   scratch += (size_t)B * sdim;
   *work_floats = npart + scratch;
   a->Sg = work ? work + npart + sg_off : nullptr;
+  // mlp_split_kernel's exchange granules, call counts and error word (the last word), when the
+  // shapes allow the split (mlp_split.inc)
+  a->hand = nullptr;
+  a->cnt = a->err = nullptr;
+  if (split_shapes(nets, sdim, B)) {
+    const int groups = 2 * ntiles;
+    const size_t ho = (*work_floats + 3) & ~(size_t)3;
+    const size_t co = ho + mlp::split_hand_floats(groups);
+    *work_floats = co + (size_t)groups + 1;
+    if (work) {
+      a->hand = work + ho;
+      a->cnt = reinterpret_cast<unsigned*>(work + co);
+      a->err = reinterpret_cast<unsigned*>(work + *work_floats - 1);
+    }
+  }
   g->ne = ne;
   g->rfirst[0] = 0;
   for (int e = 0; e < ne; e++) g->rfirst[e + 1] = g->rfirst[e] + (g->e[e].n + 63) / 64;
@@ -924,9 +950,22 @@ int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int 
   if (!attr_set) {
     HIPCHK(hipFuncSetAttribute((const void*)mlp::mlp_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                150 * 1024));  // (+ its static LDS)
+    HIPCHK(hipFuncSetAttribute((const void*)mlp::mlp_split_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL(mlp::mlp_rows_kernel, dim3(g.ntiles, 2), dim3(mlp::NT), lds, (hipStream_t)stream, a);
+  // the column-split kernel where the shapes allow it (its exchange region is in the work
+  // space); PIANORL_MLP_SPLIT=0 selects the one-workgroup-per-tile kernel
+  const char* sv = getenv("PIANORL_MLP_SPLIT");
+  if (a.hand && !(sv && sv[0] == '0')) {
+    const size_t slds = mlp::split_lds_floats(((sdim + 15) & ~15) + 4) * sizeof(float);
+    if (slds > 160 * 1024) return fail("prl_mlp_step: split kernel LDS over 160 KB");
+    const int groups = 2 * g.ntiles;
+    hipLaunchKernelGGL(mlp::mlp_split_kernel, dim3(32 * ((groups + 7) / 8)), dim3(mlp::ST), slds,
+                       (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL(mlp::mlp_rows_kernel, dim3(g.ntiles, 2), dim3(mlp::NT), lds, (hipStream_t)stream, a);
+  }
   HIPCHK(hipGetLastError());
   const int waves = g.ntw + g.rfirst[g.ne];
   hipLaunchKernelGGL(mlp::mlp_grad_kernel, dim3((waves + mlp::GWV - 1) / mlp::GWV), dim3(mlp::GWV * 64), 0,

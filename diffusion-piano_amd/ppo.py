@@ -437,6 +437,12 @@ class FusedStep:
         self.nets[train] = nets
         return nets
 
+    def mlp_error(self, B):
+        """The column-split rows kernel's error word for minibatches of B rows (0: every exchange
+        completed; 1 + e: a wait on exchange e timed out and that step's outputs are garbage)."""
+        w = self.bufs.get(B, {}).get("_mlp_work")
+        return 0 if w is None else int(w[-1:].view(torch.int32).item())
+
     def _mlp_ok(self, B):
         if not self.mfma or B > self.MFMA_MAX_ROWS:
             return False
@@ -455,7 +461,8 @@ class FusedStep:
             nets = self._mlp_nets(train)
             if "_mlp_work" not in b:
                 n = R.prl_mlp_step_work(nets, sdim, B)
-                b["_mlp_work"] = torch.empty(max(int(n), 1), device=ag.device, dtype=torch.float32)
+                # zeroed once: the column-split kernel's exchange counters start at 0 (include/pianorl.h)
+                b["_mlp_work"] = torch.zeros(max(int(n), 1), device=ag.device, dtype=torch.float32)
             w = b["_mlp_work"]
             lr_ptr = (ag._log_row if log_row is None else log_row).data_ptr()
             fl = getattr(ag, "flat", None)
@@ -486,7 +493,8 @@ class FusedStep:
             nets = self._mlp_nets(train)
             if "_mlp_work" not in b:
                 n = R.prl_mlp_step_work(nets, sdim, B)
-                b["_mlp_work"] = torch.empty(max(int(n), 1), device=ag.device, dtype=torch.float32)
+                # zeroed once: the column-split kernel's exchange counters start at 0 (include/pianorl.h)
+                b["_mlp_work"] = torch.zeros(max(int(n), 1), device=ag.device, dtype=torch.float32)
             w = b["_mlp_work"]
             chk(R.prl_mlp_step(nets, b["S"].data_ptr(), sdim, b["A"].data_ptr(), adim, b["LP"].data_ptr(),
                                b["ADV"].data_ptr(), b["RET"].data_ptr(), B, float(ag.epsilon), float(ag.entropy_coef),

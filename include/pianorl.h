@@ -128,7 +128,12 @@ int prl_colsums(int n, const float* const* src, const int* cols, const float* sc
  * nets[1] = critic (head 1). Gradients are written (not accumulated) to the d* pointers;
  * log_row [6] = the means of actor loss rows, critic squared errors, entropy, value, return,
  * advantage. Dropout masks are prl_lnrelu_fwd's (seed, *step, layer, row, column). All
- * pointers device; nets is a host array. work: prl_mlp_step_work(nets, sdim, B) floats. */
+ * pointers device; nets is a host array. work: prl_mlp_step_work(nets, sdim, B) floats, ZEROED
+ * before its first call and then kept between calls: for B <= 256, state width <= 384 and
+ * hidden widths of 128 or 256 its tail holds the column-split rows kernel's tagged exchange
+ * slices and per-tile call counts (4 workgroups per 16-row tile and network, six exchanges per
+ * step; PIANORL_MLP_SPLIT=0 selects the one-workgroup-per-tile kernel), and its last word is
+ * that kernel's error word (0, or 1 + the exchange whose bounded wait timed out). */
 typedef struct {
   int in, out;
   const float *W, *b, *gamma, *beta;  /* W [out][in]; gamma/beta: NULL on the output layer */

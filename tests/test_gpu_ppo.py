@@ -305,6 +305,58 @@ def test_fused_step_large_minibatch(ppo, tmp_path, mfma):
             np.testing.assert_allclose(g0, g1, rtol=0, atol=2e-4 * max(np.abs(g1).max(), 1e-6), err_msg=f"{net}.{k}")
 
 
+def _split_agent(ppo, tmp_path, S, B, train_critic):
+    rng = np.random.RandomState(11)
+    n = 2 * B
+    args = (rng.rand(n, S).astype(np.float32), rng.uniform(-1, 1, (n, 45)).astype(np.float32), rng.rand(n),
+            rng.uniform(-60, -40, n).astype(np.float32), rng.rand(n, S).astype(np.float32),
+            (rng.rand(n) < 0.1).astype(np.float32))
+    torch.manual_seed(0)
+    ag = ppo.PPOAgent(S, 45, batch_size=B, ppo_epochs=1, use_wandb=False, checkpoint_dir=str(tmp_path), graphs=False,
+                      fused=True)
+    ag.critic.train() if train_critic else ag.critic.eval()
+    ag._prepare(*args)
+    ag._fused = ppo.FusedStep(ag)
+    return ag, torch.randperm(n, generator=torch.Generator().manual_seed(2))[:B].cuda()
+
+
+def _grads(ag):
+    return {f"{net}.{k}": p.grad.detach().cpu().numpy().copy()
+            for net in ("actor", "critic") for k, p in getattr(ag, net).named_parameters()}
+
+
+@pytest.mark.parametrize("B,train_critic", [(128, False), (128, True), (40, True), (256, False)])
+def test_split_rows_kernel_matches_tile_kernel(ppo, tmp_path, monkeypatch, B, train_critic):
+    """The column-split rows kernel (4 workgroups per 16-row tile and network, six exchanges per
+    step; csrc/mlp_split.inc) against the one-workgroup-per-tile kernel (PIANORL_MLP_SPLIT=0) on
+    the same weights, minibatch and dropout masks: the GEMMs run in the same k order, only the
+    LayerNorm row sums and column sums are added in another order, so the logged sums agree to
+    1e-5 relative and every gradient to 1e-4 of its tensor's largest entry (measured: <= 5.5e-5,
+    a LayerNorm beta gradient summed over 256 rows with cancellation). The state width 329
+    is the piano observation's (unaligned weight rows), B = 40 a ragged last tile, B = 256 the
+    split's row limit (128 workgroups). Three split steps in a row are bitwise equal (the
+    monotonic exchange counters carry over calls) and the error word stays 0."""
+    ag, idx = _split_agent(ppo, tmp_path, 329, B, train_critic)
+    out = {}
+    for mode in ("0", "1", "1", "1"):
+        monkeypatch.setenv("PIANORL_MLP_SPLIT", mode)
+        step0 = ag._fused.step.clone()
+        ag._forward_backward(idx, ag._log_row)
+        torch.cuda.synchronize()
+        ag._fused.step.copy_(step0)  # the same dropout draw for every run
+        out.setdefault(mode, []).append((ag._log_row.cpu().numpy().copy(), _grads(ag)))
+    assert ag._fused.mlp_error(B) == 0
+    (row0, g0), = out["0"]
+    for row1, g1 in out["1"][1:]:
+        np.testing.assert_array_equal(row1, out["1"][0][0])
+        for k in g1:
+            np.testing.assert_array_equal(g1[k], out["1"][0][1][k], err_msg=k)
+    row1, g1 = out["1"][0]
+    np.testing.assert_allclose(row1, row0, rtol=1e-5, atol=1e-7)
+    for k in g0:
+        np.testing.assert_allclose(g1[k], g0[k], rtol=0, atol=1e-4 * max(np.abs(g0[k]).max(), 1e-6), err_msg=k)
+
+
 def test_rollout_trainer_masks_auto_reset_steps(ppo, tmp_path):
     """An auto-reset step (FIRST: the kernel ignored the action and reset the env) is not a
     transition: the horizon rollout marks it invalid and _prepare drops it after GAE (it enters
