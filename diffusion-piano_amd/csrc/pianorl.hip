@@ -718,10 +718,10 @@ int prl_colsums(int n, const float* const* src, const int* cols, const float* sc
 
 // ---------------------------------------------------------------- fused minibatch step on the matrix cores (mlp_step.inc)
 namespace {
-// the column-split rows kernel's shape conditions: <= 256 rows, state width <= 384, hidden
+// the column-split rows kernel's shape conditions: <= 256 rows, state width 32..384, hidden
 // widths 128 or 256 (mlp_split.inc)
 bool split_shapes(const prl_net* nets, int sdim, int B) {
-  if (B > mlp::SPLIT_MAX_ROWS || sdim > mlp::SPLIT_MAX_SDIM) return false;
+  if (B > mlp::SPLIT_MAX_ROWS || sdim > mlp::SPLIT_MAX_SDIM || sdim < 32) return false;
   for (int i = 0; i < 2; i++)
     for (int l = 0; l + 1 < nets[i].nlayers; l++)
       if (nets[i].layer[l].out != 128 && nets[i].layer[l].out != 256) return false;

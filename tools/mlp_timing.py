@@ -37,11 +37,12 @@ t = np.array(out[:], dtype=np.int64).reshape(2, 32)
 names = {0: "start", 21: "L0 gemm", 1: "fwd L0", 22: "L1 gemm", 2: "fwd L1", 23: "L2 gemm", 3: "fwd L2", 5: "out+head", 7: "out dX",
          8: "L2 ln-bwd", 11: "L2 dX", 12: "L1 ln-bwd", 15: "L1 dX", 16: "L0 ln-bwd", 19: "L0", 20: "end",
          # mlp_split_kernel (member 0 of tile 0): the exchanges' signal -> data-in-LDS spans
+         30: "idx rows", 31: "state tile", 4: "out gemm",
          24: "x0 exch", 25: "x1 exch", 26: "x2 exch", 27: "x3 exch", 28: "x4 exch", 29: "x5 exch"}
 for net in range(2):
     prev = t[net, 0]
     print("actor" if net == 0 else "critic", "total", t[net, 20] - t[net, 0], "cycles")
-    order = [0, 21, 24, 1, 22, 25, 2, 23, 26, 3, 5, 7, 27, 8, 11, 28, 12, 15, 29, 16, 19, 20]
+    order = [0, 30, 31, 21, 24, 1, 22, 25, 2, 23, 26, 3, 4, 5, 7, 27, 8, 11, 28, 12, 15, 29, 16, 19, 20]
     for i in order:
         if i == 0 or t[net, i] == 0:
             continue

@@ -46,6 +46,8 @@ def main():
     p.add_argument("--blas", default="default", choices=["default", "rocblas", "hipblaslt"])
     p.add_argument("--no-tune", action="store_true", help="no TunableOp GEMM selection")
     p.add_argument("--autograd", action="store_true", help="torch autograd minibatch step instead of FusedStep")
+    p.add_argument("--hand", default="hull", choices=["hull", "primitive", "authored"],
+                   help="collider set (bench.py HANDS; default: the reference's default colliders)")
     args = p.parse_args()
 
     import torch
@@ -63,9 +65,12 @@ def main():
     dp = importlib.import_module("diffusion-piano_amd")
     ppo = importlib.import_module("diffusion-piano_amd.ppo")
     sharding = importlib.import_module("diffusion-piano_amd.sharding")
-    from bench import load_song
+    import dataclasses
+
+    from bench import HANDS, load_song
 
     seq, task = load_song(dp, args.song)
+    task = dataclasses.replace(task, primitive_fingertip_collisions=HANDS[args.hand][0])
     shard = sharding.shard_envs(args.envs * world, rank, world)
     env = dp.BatchedPianoEnv(shard.count, seq, task, device=dev, seed=12345,
                              env_offset=shard.start)
@@ -119,6 +124,7 @@ def main():
             "warmup": args.warmup, "ms_per_iter": elapsed / args.iters * 1e3, "higher_is_better": True,
             "scaling": "weak", "dtype": "f32", "data": "synthetic: env rollouts of the policy, random init",
             "config": {"workload": f"ppo_v2 {args.mode} loop, {args.envs} envs/GPU {args.song}",
+                       "hand": f"{args.hand}: {HANDS[args.hand][2]}",
                        "mode": args.mode, "envs_per_gpu": args.envs, "batch": args.batch, "epochs": args.epochs,
                        "horizon": args.horizon if args.mode == "rollout" else 1,
                        "minibatch_steps_per_update": nmb * args.epochs, "graphs": not args.eager,
