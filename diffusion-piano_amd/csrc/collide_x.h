@@ -23,6 +23,7 @@ struct XShape {
   f3 e0, e1;       // hull: an enclosing capsule (world), radius er
   float er;
   const uint64_t* cells;  // hull: its support cells (DevModel::x_cell), or nullptr: scan all vertices
+  const float4* cellv;    // hull: its support-cell vertex table (DevModel::x_cellv), or nullptr
 };
 
 // a collider moved by -o (its centre, segment and enclosing capsule; rotations, half sizes and
@@ -109,6 +110,28 @@ inline void hull_support_cells(const double (*v)[3], int n, uint64_t* out) {
       }
 }
 
+// The support-cell vertex table of a hull (DevModel::x_cellv) from its cells' masks: per cell the
+// candidates' fp32 coordinates in ascending vertex order, padded with the last candidate (a
+// repeat never wins the first-maximal search), and cell XNCELL = vertex 0 (the zero direction).
+// false when a cell holds more than XCV candidates (or none): the mask scan is used instead.
+inline bool hull_cell_table(const double (*v)[3], const uint64_t* cells, float (*out)[XCV][4]) {
+  for (int c = 0; c <= XNCELL; c++) {
+    uint64_t msk = c < XNCELL ? cells[c] : 1ull;
+    const int cnt = __builtin_popcountll(msk);
+    if (cnt < 1 || cnt > XCV) return false;
+    int k = 0, last = 0;
+    while (msk) {
+      last = __builtin_ctzll(msk);
+      msk &= msk - 1ull;
+      for (int j = 0; j < 3; j++) out[c][k][j] = (float)v[last][j];
+      out[c][k++][3] = 0.f;
+    }
+    for (; k < XCV; k++)
+      for (int j = 0; j < 4; j++) out[c][k][j] = out[c][k - 1][j];
+  }
+  return true;
+}
+
 // support cell of a (local) direction: the cube-map face of its largest component, the cell of
 // its two tangent ratios over [-1, 1] (hull_support_cells above builds the tables with
 // the same convention; its cells are grown, so rounding at a cell edge picks a cell that still
@@ -139,6 +162,22 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
   f3 loc;
   if (s.type == PS_GEOM_BOX) {
     loc = mk3(sgn0f(dl.x) * s.hs.x, sgn0f(dl.y) * s.hs.y, sgn0f(dl.z) * s.hs.z);
+  } else if (s.cellv) {
+    // the first maximal vertex over the direction's cell's candidates (x_cellv: the same
+    // candidates as x_cell's mask, in the same order, padded by repeats): the cell's 128 bytes
+    // in one round of reads, then the same compares as the mask scan below - the same vertex
+    const bool zero = dl.x == 0.f && dl.y == 0.f && dl.z == 0.f;
+    const float4* t = s.cellv + (zero ? XNCELL : hull_cell(dl)) * XCV;
+    float4 v[XCV];
+#pragma unroll
+    for (int u = 0; u < XCV; u++) v[u] = t[u];
+    float bd = -INFINITY;
+    loc = mk3(0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < XCV; u++) {
+      const float p = fmaf(dl.z, v[u].z, fmaf(dl.y, v[u].y, dl.x * v[u].x));
+      if (p > bd) { bd = p; loc = mk3(v[u].x, v[u].y, v[u].z); }
+    }
   } else if (s.cells) {
     // the first maximal vertex over the candidates of the direction's support cell (x_cell, its
     // bits in ascending vertex order, four per trip: their reads issued together) - the same
@@ -208,6 +247,27 @@ __device__ __forceinline__ MprPt mpr_sup(const DevModel* __restrict__ m, const X
   p.v = p.a - p.b;
   return p;
 }
+// Paired MPR (PAIR = true): the two lanes 2k, 2k + 1 of a wave run the same pair in lockstep -
+// every portal step computed by both, identically - and split each step's two support
+// searches: lane 2k searches A along d, lane 2k + 1 searches B along -d (O = its own collider,
+// role = lane & 1), and the points cross over by DPP. The two searches' dependent L2 reads
+// (support cell, then its vertices) overlap instead of running one after the other; the
+// points are the same bits as mpr_sup's (same function, same arguments).
+__device__ __forceinline__ float xchg1(float v) {  // the value of lane ^ 1 (quad_perm [1, 0, 3, 2])
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+template <bool PAIR>
+__device__ __forceinline__ MprPt mpr_sup_t(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
+                                           const XShape& O, bool role, f3 d) {
+  if (!PAIR) return mpr_sup(m, A, B, d);
+  const f3 mine = x_support(m, O, role ? d * -1.f : d);
+  const f3 oth = mk3(xchg1(mine.x), xchg1(mine.y), xchg1(mine.z));
+  MprPt p;
+  p.a = role ? oth : mine;
+  p.b = role ? mine : oth;
+  p.v = p.a - p.b;
+  return p;
+}
 __device__ __forceinline__ f3 portal_dir(const MprPt& p1, const MprPt& p2, const MprPt& p3) {
   return nrmz3(cross3(p2.v - p1.v, p3.v - p1.v));
 }
@@ -261,14 +321,18 @@ __device__ __forceinline__ f3 mpr_pos(const MprPt& p0, const MprPt& p1, const Mp
   const f3 pb = p0.b * b0 + p1.b * b1 + p2.b * b2 + p3.b * b3;
   return (pa * inv + pb * inv) * 0.5f;
 }
-// 1: penetrating (depth >= 0, normal A -> B, contact point); 0: apart
+// 1: penetrating (depth >= 0, normal A -> B, contact point); 0: apart. PAIR: paired lanes (O,
+// role: see mpr_sup_t)
+template <bool PAIR = false>
 __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
-                                               float* depth, f3* n, f3* pos, int* its = nullptr) {
+                                               float* depth, f3* n, f3* pos, int* its = nullptr,
+                                               const XShape* O = nullptr, bool role = false) {
+  const XShape& own = PAIR ? *O : A;
   MprPt p0, p1, p2, p3;
   p0.a = A.c; p0.b = B.c; p0.v = A.c - B.c;
   if (p0.v.x == 0.f && p0.v.y == 0.f && p0.v.z == 0.f) p0.v.x += 10.f * MPR_EPSF;
   f3 dir = nrmz3(p0.v * -1.f);
-  p1 = mpr_sup(m, A, B, dir);
+  p1 = mpr_sup_t<PAIR>(m, A, B, own, role, dir);
   float dt = dot3(p1.v, dir);
   if (mpr_zero(dt) || dt < 0.f) return 0;
   dir = cross3(p0.v, p1.v);
@@ -279,7 +343,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
     return 1;
   }
   dir = nrmz3(dir);
-  p2 = mpr_sup(m, A, B, dir);
+  p2 = mpr_sup_t<PAIR>(m, A, B, own, role, dir);
   dt = dot3(p2.v, dir);
   if (mpr_zero(dt) || dt < 0.f) return 0;
   dir = nrmz3(cross3(p1.v - p0.v, p2.v - p0.v));
@@ -287,7 +351,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
   for (int it = 0;; it++) {
     if (its) ++*its;  // (timing build: support calls of the refinement)
     if (it > 4 * MPR_MAXITF) return 0;
-    p3 = mpr_sup(m, A, B, dir);
+    p3 = mpr_sup_t<PAIR>(m, A, B, own, role, dir);
     dt = dot3(p3.v, dir);
     if (mpr_zero(dt) || dt < 0.f) return 0;
     bool cont = false;
@@ -306,7 +370,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
     dir = portal_dir(p1, p2, p3);
     dt = dot3(p1.v, dir);
     if (mpr_zero(dt) || dt > 0.f) break;
-    const MprPt v4 = mpr_sup(m, A, B, dir);
+    const MprPt v4 = mpr_sup_t<PAIR>(m, A, B, own, role, dir);
     const float d4 = dot3(v4.v, dir);
     if (!(mpr_zero(d4) || d4 > 0.f) || portal_reach_tol(p1, p2, p3, v4, dir)) return 0;
     expand_portal(p0, p1, p2, p3, v4);
@@ -314,7 +378,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
   for (int it = 0;; it++) {
     if (its) ++*its;  // (timing build: support calls of the refinement)
     dir = portal_dir(p1, p2, p3);
-    const MprPt v4 = mpr_sup(m, A, B, dir);
+    const MprPt v4 = mpr_sup_t<PAIR>(m, A, B, own, role, dir);
     if (portal_reach_tol(p1, p2, p3, v4, dir) || it > MPR_MAXITF) {
       const f3 cp = tri_closest_origin(p1.v, p2.v, p3.v);
       *depth = norm3(cp);
@@ -560,9 +624,10 @@ __device__ __forceinline__ bool x_apart(const XShape& A, const XShape& B) {
 // Narrow phase of collider A (geom1) with collider B: capsule-box (the box becomes geom1:
 // swap = true, normal box -> capsule), box-box, or MPR for every pair with a hull. Returns the
 // contact count (<= 4); normals point geom1 -> geom2.
+template <bool PAIR = false>
 __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
                                         f3 (&pos)[BB_MAXPT], float (&dist)[BB_MAXPT], f3 (&nrm)[BB_MAXPT], bool& swap,
-                                        int* its = nullptr) {
+                                        int* its = nullptr, const XShape* O = nullptr, bool role = false) {
   swap = false;
   if (A.type == 0 && B.type == PS_GEOM_BOX) {
     swap = true;
@@ -577,7 +642,7 @@ __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XS
   }
   float depth;
   f3 n, p;
-  const int cnt = mpr_penetration(m, A, B, &depth, &n, &p, its);
+  const int cnt = mpr_penetration<PAIR>(m, A, B, &depth, &n, &p, its, O, role);
   if (n.x == 0.f && n.y == 0.f && n.z == 0.f) n = mk3(0.f, 0.f, 1.f);
   pos[0] = p;
   nrm[0] = n;
@@ -589,13 +654,17 @@ __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XS
 // portal arithmetic at the pair's scale (centimetres) instead of world coordinates (~0.5 m: an
 // fp32 ulp of 6e-8 m on every support point, against MPR's 1e-6 m tolerance, steers the portal
 // differently from the fp64 checker's); the contact points back in world coordinates
+// (PAIR: called by both lanes of a pair with the same A, B; role = lane & 1)
+template <bool PAIR = false>
 __device__ __forceinline__ int x_narrow_local(const DevModel* __restrict__ m, XShape A, XShape B, f3 (&pos)[BB_MAXPT],
                                               float (&dist)[BB_MAXPT], f3 (&nrm)[BB_MAXPT], bool& swap,
-                                              int* its = nullptr) {
+                                              int* its = nullptr, bool role = false) {
   const f3 org = B.c;
   x_shift(A, org);
   x_shift(B, org);
-  const int cnt = x_narrow(m, A, B, pos, dist, nrm, swap, its);
+  XShape O;
+  if (PAIR) O = role ? B : A;
+  const int cnt = x_narrow<PAIR>(m, A, B, pos, dist, nrm, swap, its, &O, role);
 #pragma unroll
   for (int j = 0; j < BB_MAXPT; j++) pos[j] = pos[j] + org;
   return cnt;

@@ -40,6 +40,7 @@ constexpr int KGEO = 16;       // floats per key collision record
 // and cell the vertices that can be the support of a direction in the cell (DevModel::x_cell)
 constexpr int XCG = 4;
 constexpr int XNCELL = 6 * XCG * XCG;
+constexpr int XCV = 8;  // candidates per cell in the support-cell vertex table (DevModel::x_cellv)
 
 struct DevModel {
   float timestep;
@@ -105,6 +106,12 @@ struct DevModel {
   // over the whole (grown) cell, so the fp32 scan over the mask finds the same first maximal
   // vertex as the scan over all of them
   uint64_t x_cell[NXT][XNCELL];
+  // hull: the same candidates' fp32 coordinates per cell (ascending vertex order, padded with the
+  // last one; cell XNCELL = vertex 0, the zero direction's): one 128-byte read per support search
+  // instead of the mask read and then the vertex reads. x_cellv_ok = 0 when a cell holds more
+  // than XCV candidates (the mask scan is used)
+  alignas(16) float x_cellv[NXT][XNCELL + 1][XCV][4];
+  int x_cellv_ok[NXT];
   int nxpairs;                 // hand-hand pairs with an extra collider: a | b << 8
   int nxpairs_same;            // leading ones within one hand (the rest cross hands)
   int xpair[PS_MAX_XPAIRS];

@@ -408,6 +408,7 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
       if (t == PS_GEOM_HULL) {
         enclosing_capsule(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_ec[e]);
         hull_support_cells(&d->hull_vert[h][d->xgeom_vert[h][i][0]], d->xgeom_vert[h][i][1], m->x_cell[e]);
+        m->x_cellv_ok[e] = hull_cell_table(&d->hull_vert[h][d->xgeom_vert[h][i][0]], m->x_cell[e], m->x_cellv[e]);
       }
     }
   for (int g = 0; g < NCOLL; g++) {

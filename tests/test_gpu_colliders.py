@@ -13,6 +13,8 @@ state with the hand joints moved by 1e-7 rad, moves by more than 1e-3 on ~8% of 
 1e-2 at most 2x the checker's own + 1%; p99 below 0.1; one substep: 1e-4 / 1e-3, p99 < 1e-2), and
 the narrow phase itself is held pair by pair (test_narrow_phase_matches_checker).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -73,6 +75,7 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
     e, f = np.concatenate(errs), np.concatenate(floor)
     assert_flip_rates(e, f, "box/hull hand, control step")
     re, rf = np.concatenate(rerr), np.concatenate(rfloor)
+    print(f"box/hull hand, control step reward: p95 {np.percentile(re, 95):.3g} floor p95 {np.percentile(rf, 95):.3g}")
     assert np.percentile(re, 95) <= max(1e-3, 2 * np.percentile(rf, 95)), (np.percentile(re, 95), np.percentile(rf, 95))
     same = np.mean(np.concatenate(ncg) == np.concatenate(nco))
     assert same > 0.9, same
@@ -162,13 +165,16 @@ def test_narrow_phase_matches_checker(dp, ref):
     checker's ref_narrow on random fingertip-scale pairs, inputs rounded to fp32 first:
     same contact count, depth within 2e-6 m, normal within 1e-3, point within 1e-4 m. The
     support search over the hulls' support cells (the step kernel's) and over all vertices give
-    bitwise the same results (the cells drop only vertices beaten by a margin over the cell)."""
+    bitwise the same results (the cells drop only vertices beaten by a margin over the cell); the
+    step kernel's paired MPR (two lanes per pair, A's and B's support searches on one lane each)
+    over the cells' vertex tables gives the mask scan's bits in the same launch and is the
+    configuration checked against the checker."""
     import ctypes as C
     from pathlib import Path
 
     from helpers import capsule_points
 
-    lib = C.CDLL(str(Path(__file__).resolve().parents[1] / "tools" / "libxcheck.so"))
+    lib = C.CDLL(os.environ.get("PS_XCHECK_LIB", str(Path(__file__).resolve().parents[1] / "tools" / "libxcheck.so")))
     lib.xcheck_run.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     rng = np.random.RandomState(11)
     _, hull = dp.mjcf.convex_hull_collider(capsule_points(0.0085, 0.006))
@@ -227,7 +233,17 @@ def test_narrow_phase_matches_checker(dp, ref):
     assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), full.data_ptr(), n, 0) == 0
     assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), out.data_ptr(), n, 1) == 0
     assert torch.equal(out, full), int((out != full).any(dim=1).sum())
-    o = out.cpu().numpy()
+    # the step kernel's configuration: paired MPR (two lanes per pair, one support search each)
+    # over the support-cell vertex tables where a hull's cells fit them (the tip hull, the
+    # cube) - bitwise the mask scan's results in the same launch shape; it is the one checked
+    # against the checker below. (Paired and one-per-lane copies of the same source differ in
+    # the last bits of ~1/5 of the pairs: the compiler fuses multiply-adds per inlined copy.)
+    paired = torch.zeros(n, 29, device="cuda:0")
+    pmask = torch.zeros(n, 29, device="cuda:0")
+    assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), paired.data_ptr(), n, 7) == 0
+    assert lib.xcheck_run(dv.data_ptr(), len(verts), dA.data_ptr(), dB.data_ptr(), pmask.data_ptr(), n, 3) == 0
+    assert torch.equal(paired, pmask), int((paired != pmask).any(dim=1).sum())
+    o = paired.cpu().numpy()
     bad, hits, counted = [], 0, 0
     for i in range(n):
         want = ref.narrow(ra[i], rb[i])
