@@ -47,6 +47,7 @@ for H in hull primitive authored; do
 done
 if [ -z "$NOPPO" ]; then
 timeout -k 10 200 python tools/ppo_bench.py --mode reference --iters 3 --warmup 2 > profiles/${P}_ppo_bench.jsonl 2>/dev/null || exit 8
+timeout -k 10 200 python tools/ppo_bench.py --mode reference --iters 3 --warmup 2 --hand authored >> profiles/${P}_ppo_bench.jsonl 2>/dev/null || exit 8
 # the PPO loop's kernels (TunableOp off: no GEMM tuning launches in the trace)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${P}_ppo_trace -- python tools/ppo_bench.py --mode reference --iters 2 --warmup 1 --no-tune > gpurun_out/${P}_ppo_trace.log 2>&1 || exit 8
 find gpurun_out/${P}_ppo_trace -name "*kernel_stats.csv" -exec cp {} profiles/${P}_ppo_kernel_stats.csv \;
