@@ -169,18 +169,8 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
     const bool zero = dl.x == 0.f && dl.y == 0.f && dl.z == 0.f;
     const float4* t = s.cellv + (zero ? XNCELL : hull_cell(dl)) * XCV;
     float4 v[XCV];
-#if PS_XCELL_GLOBAL  // (global, not flat, loads of the table: vmcnt only)
-    typedef float xv4 __attribute__((ext_vector_type(4)));
-    typedef const __attribute__((address_space(1))) xv4 gxv4;
-#pragma unroll
-    for (int u = 0; u < XCV; u++) {
-      const xv4 q = ((gxv4*)t)[u];
-      v[u] = make_float4(q[0], q[1], q[2], q[3]);
-    }
-#else
 #pragma unroll
     for (int u = 0; u < XCV; u++) v[u] = t[u];
-#endif
     float bd = -INFINITY;
     loc = mk3(0.f, 0.f, 0.f);
 #pragma unroll
@@ -242,9 +232,6 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
   return s.c + mv3(s.R, loc);
 }
 
-#ifndef PS_XCELL_GLOBAL
-#define PS_XCELL_GLOBAL 0
-#endif
 // ------------------------------------------------------------------ MPR
 constexpr float MPR_TOLF = 1e-6f;
 constexpr int MPR_MAXITF = 50;
