@@ -41,11 +41,11 @@ def bytes_per_env_step(obs_dim):
 
 # collider sets: TaskConfig.primitive_fingertip_collisions value, kernel instantiation, description
 HANDS = {
-    "hull": (False, "pianosim_kernel<true>", "palm boxes + convex-hull distal colliders: the reference's default "
+    "hull": (False, "pianosim_kernel<true, 2>", "palm boxes + convex-hull distal colliders: the reference's default "
                                              "PianoTask(primitive_fingertip_collisions=False)"),
-    "primitive": (True, "pianosim_kernel<true>", "palm boxes + capsule distal colliders: the reference's "
+    "primitive": (True, "pianosim_kernel<true, 2>", "palm boxes + capsule distal colliders: the reference's "
                                                  "PianoTask(primitive_fingertip_collisions=True)"),
-    "authored": (None, "pianosim_kernel<false>", "all-capsule authored hand (no reference counterpart)"),
+    "authored": (None, "pianosim_kernel<false, 2>", "all-capsule authored hand (no reference counterpart)"),
 }
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -342,17 +342,20 @@ def main():
     if not args.no_legs:
         # the same workload (envs, actions, K, W) with the other collider sets, after the main
         # timed region; top-level keys of the line (the driver's parsed record keeps them)
-        for hand in HANDS:
-            if hand == args.hand:
-                continue
-            lenv = dp.BatchedPianoEnv(shard.count, seq, hand_task(hand), device=dev, seed=12345, env_offset=shard.start)
+        # and the timed hand with the refining Newton step on coupled substeps (solver_refine=1)
+        runs = [(h, h, hand_task(h)) for h in HANDS if h != args.hand]
+        runs.append(("refined", args.hand, dataclasses.replace(hand_task(args.hand), solver_refine=1)))
+        for key, hand, ltask in runs:
+            lenv = dp.BatchedPianoEnv(shard.count, seq, ltask, device=dev, seed=12345, env_offset=shard.start)
             lenv.reset()
             stagger_episodes(lenv, shard.start, lenv.song.T)
             l_elapsed, l_kernel_ms = timed_rollout(lenv, actions, args.steps, args.warmup, dev,
                                                    sharding.EpisodeReturns(N, dev), sharding)
-            legs[hand] = {"value": total_steps / l_elapsed, "ms_per_step": l_elapsed / args.steps * 1e3,
-                          "kernel_ms_avg": l_kernel_ms, "unit": "env-steps/s", "hand": HANDS[hand][2],
-                          "kernel": HANDS[hand][1]}
+            legs[key] = {"value": total_steps / l_elapsed, "ms_per_step": l_elapsed / args.steps * 1e3,
+                         "kernel_ms_avg": l_kernel_ms, "unit": "env-steps/s", "hand": HANDS[hand][2],
+                         "kernel": HANDS[hand][1]}
+            if key == "refined":
+                legs[key]["solver_refine"] = 1
             lenv.close()
     if rank == 0:
         sha = lib_sha()
@@ -407,6 +410,8 @@ def main():
             line["capsule_hand"] = legs["authored"]
         if "hull" in legs:
             line["reference_default_hand"] = legs["hull"]
+        if "refined" in legs:  # TaskConfig(solver_refine=1): tighter fp32 parity
+            line["refined_solve"] = legs["refined"]
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"] = cpu_baseline(dp, seq, hand_task(args.hand), args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(line), flush=True)

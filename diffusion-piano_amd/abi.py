@@ -116,7 +116,7 @@ class TaskCfg(C.Structure):
     _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
                 ("wrong_press_termination", i32), ("energy_penalty_coef", d),
                 ("solver_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32),
-                ("solver", i32), ("randomize_hand_positions", i32)]
+                ("solver", i32), ("randomize_hand_positions", i32), ("solver_refine", i32)]
 
 
 SOLVER_EXACT = SOLVER_NEWTON = 1

@@ -59,6 +59,8 @@ struct ps_env {
   float* park;              // [N][PARK_WORDS][64] kernel scratch (lane state around the Newton solve)
   uint64_t seed;
   bool has_x;               // box / hull colliders: the pianosim_kernel<true> instantiation
+  int wave_slots;           // SIMDs of the device: a step launch of at most this many envs runs one
+                            // wave per SIMD and takes the one-wave (no-scratch) instantiation
   Contact* con_out;         // [N][MAXCON] contact lists of the last step (ps_record_contacts)
 };
 
@@ -535,6 +537,7 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   if (cfg->n_steps_lookahead < 0) return fail("negative lookahead");
   if (cfg->max_contacts < 0 || cfg->max_contacts > MAXCON) return fail("max_contacts out of range");
   if (cfg->solver_iterations < 0) return fail("negative solver_iterations");
+  if (cfg->solver_refine < 0 || cfg->solver_refine > 2) return fail("solver_refine must be 0, 1 or 2");
   if (cfg->solver != PS_SOLVER_NEWTON) return fail("unknown solver (PS_SOLVER_NEWTON is the only one)");
   for (int t = 0; t < song->T; t++) {
     if (song->count[t] < 0 || song->count[t] > PS_MAX_NOTES) return fail("bad note count");
@@ -615,6 +618,13 @@ int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_tas
   E->applied_on = false;
   E->ordered = !(getenv("PIANOSIM_NO_ORDER") && atoi(getenv("PIANOSIM_NO_ORDER")));
   E->full_cpl = getenv("PIANOSIM_DEBUG_FULL_COUPLED") && atoi(getenv("PIANOSIM_DEBUG_FULL_COUPLED"));
+  {
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    E->wave_slots = 4 * cus;  // 4 SIMDs per CDNA compute unit
+    const char* w = getenv("PIANOSIM_ONE_WAVE_MAX");  // (A/B runs: the threshold; 0 never)
+    if (w) E->wave_slots = atoi(w);
+  }
   *out = E;
   return 0;
 }
@@ -678,7 +688,8 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
   Cfg cfg{E->cfg.n_steps_lookahead, E->cfg.fingering_reward, E->cfg.forearm_reward, E->cfg.wrong_press_termination,
           E->cfg.solver_iterations, E->cfg.max_contacts, E->obs_dim, E->cfg.canonical_actions,
           (float)E->cfg.energy_penalty_coef, E->cfg.randomize_hand_positions != 0,
-          (uint32_t)E->seed, (uint32_t)(E->seed >> 32), (uint32_t)E->env_offset, E->full_cpl};
+          (uint32_t)E->seed, (uint32_t)(E->seed >> 32), (uint32_t)E->env_offset, E->full_cpl,
+          E->cfg.solver_refine};
   Bufs b{E->qpos, E->qvel, E->qws, E->ctrl, E->sustain, E->t_idx, E->last,
          E->applied_on ? E->applied : nullptr, E->terms, E->tips, E->ncon, E->mus_acc, E->mus_ep, E->mus_cnt,
          E->hand_dy, E->episode, E->stats, E->con_out, E->warnings, E->park};
@@ -689,12 +700,18 @@ static int launch(ps_env* E, int mode, const float* action, const uint8_t* mask,
     HIPCHK(hipGetLastError());
     order = E->order;
   }
-  if (E->has_x)
-    hipLaunchKernelGGL(pianosim_kernel<true>, dim3(E->n), dim3(64), PS_LAUNCH_LDS, (hipStream_t)stream, E->d_model, song, cfg, b,
-                       action, mask, obs, reward, discount, step_type, mode, E->n, order);
-  else
-    hipLaunchKernelGGL(pianosim_kernel<false>, dim3(E->n), dim3(64), PS_LAUNCH_LDS, (hipStream_t)stream, E->d_model, song, cfg, b,
-                       action, mask, obs, reward, discount, step_type, mode, E->n, order);
+  // at most one wave per SIMD: the instantiation built for one resident wave (its spills in
+  // AGPRs, no scratch traffic) - the two-wave build's second slot would stay empty anyway
+  const bool one = E->n <= E->wave_slots;
+#define PS_LAUNCH(XG, WPE)                                                                                    \
+  hipLaunchKernelGGL((pianosim_kernel<XG, WPE>), dim3(E->n), dim3(64), PS_LAUNCH_LDS, (hipStream_t)stream, \
+                     E->d_model, song, cfg, b, action, mask, obs, reward, discount, step_type, mode, E->n, order)
+  if (E->has_x) {
+    if (one) PS_LAUNCH(true, 1); else PS_LAUNCH(true, PS_WAVES_PER_EU);
+  } else {
+    if (one) PS_LAUNCH(false, 1); else PS_LAUNCH(false, PS_WAVES_PER_EU);
+  }
+#undef PS_LAUNCH
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -102,6 +102,10 @@ class TaskConfig:
     # substep (None: the library default, 24). The round-1 truncated "pgs" is retired.
     constraint_solver: str = "newton"
     solver_iterations: Optional[int] = None
+    # 0: the solve ends when its line search ends in the Hessian's piece (the exact minimiser, to
+    # the fp32 factor's error); 1: one more Newton step in that piece on coupled-hand substeps;
+    # 2: on every substep (tighter fp32 parity for ~5-8% of the throughput; ps_task_cfg.solver_refine)
+    solver_refine: int = 0
     max_contacts: int = 20
     hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
     # PianoTask keyword arguments (tasks/base.py:96-107, forwarded by PianoWithShadowHands'
@@ -169,6 +173,9 @@ def compile_task(midi, cfg: TaskConfig, canonical_actions: bool = True):
                          " (the round-1 truncated 'pgs' solver is retired)")
     tc.solver = abi.SOLVER_NEWTON
     tc.solver_iterations = 0 if cfg.solver_iterations is None else int(cfg.solver_iterations)
+    if cfg.solver_refine not in (0, 1, 2):
+        raise ValueError(f"solver_refine must be 0, 1 or 2, got {cfg.solver_refine!r}")
+    tc.solver_refine = int(cfg.solver_refine)
     tc.randomize_hand_positions = int(cfg.randomize_hand_positions)
     tc.max_contacts = min(cfg.max_contacts, abi.MAX_CONTACTS_LIMIT)
     tc.canonical_actions = int(canonical_actions)

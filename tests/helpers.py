@@ -23,11 +23,13 @@ def song(dp, name):
 
 def tool_hand_kwargs():
     """TaskConfig kwargs of the collider set a development tool runs (PIANOSIM_HAND = hull |
-    primitive | authored, bench.py --hand; PIANOSIM_HULL=1 = hull; default the all-capsule hand)."""
+    primitive | authored, bench.py --hand; PIANOSIM_HULL=1 = hull; default the all-capsule hand)
+    and its Newton refinement (PIANOSIM_REFINE = TaskConfig.solver_refine, default 0)."""
     import os
     h = os.environ.get("PIANOSIM_HAND") or ("hull" if os.environ.get("PIANOSIM_HULL") else "authored")
-    return {"hull": {"primitive_fingertip_collisions": False}, "primitive": {"primitive_fingertip_collisions": True},
-            "authored": {}}[h]
+    kw = {"hull": {"primitive_fingertip_collisions": False}, "primitive": {"primitive_fingertip_collisions": True},
+          "authored": {}}[h]
+    return dict(kw, solver_refine=int(os.environ.get("PIANOSIM_REFINE", "0")))
 
 
 def random_states(md, n, rng, vscale=0.5):

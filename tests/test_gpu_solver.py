@@ -88,9 +88,10 @@ def test_solver_stats_and_caps(dp):
     assert st[..., 3].max() <= 96
 
 
-def _replay(dp, ref, select, steps=14, N=2048, seed=7):
-    """Roll N GPU envs; replay on the oracle the env-steps `select(stats, state)` picks."""
-    md, g, _ = _pair(dp, ref, "crossing_field", N)
+def _replay(dp, ref, select, steps=14, N=2048, seed=7, **kw):
+    """Roll N GPU envs; replay on the oracle the env-steps `select(stats, state)` picks (kw: more
+    TaskConfig options of the GPU env)."""
+    md, g, _ = _pair(dp, ref, "crossing_field", N, **kw)
     lo, hi = dp_action_spec(md)
     rng = np.random.RandomState(seed)
     g.reset()
@@ -135,6 +136,22 @@ def test_newton_coupled_hands(dp, ref):
     n, e, f = _replay(dp, ref, lambda st: st[:, 4] >= 10)
     assert n >= 16, f"only {n} coupled env-steps"
     assert_parity(e, f, "coupled env-steps")
+
+
+def test_solver_refine_coupled_hands(dp, ref):
+    """TaskConfig(solver_refine=1): one more Newton step in the converged piece on coupled
+    substeps. The coupled replays then meet the 1e-4 target over ALL env-steps (p99 ceiling 1e-4
+    instead of PARITY_P99_CEIL; default solve: 1.6e-4, refined: ~8e-5)."""
+    n, e, f = _replay(dp, ref, lambda st: st[:, 4] >= 10, solver_refine=1)
+    assert n >= 16, f"only {n} coupled env-steps"
+    assert_parity(e, f, "coupled env-steps, solver_refine=1", p99_ceil=1e-4)
+
+
+def test_solver_refine_heavy_states(dp, ref):
+    """The same on the heavy-contact replays with every substep refined (solver_refine=2)."""
+    n, e, f = _replay(dp, ref, lambda st: st[:, 3] > 40, solver_refine=2)
+    assert n >= 4, f"only {n} heavy env-steps"
+    assert_parity(e, f, "heavy env-steps, solver_refine=2", p99_ceil=1e-4)
 
 
 def test_newton_coupled_hands_full_block(dp, ref, monkeypatch):

@@ -55,7 +55,17 @@ def test_pgs_solver_is_retired(dp):
     with pytest.raises(ValueError, match="retired"):
         dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(constraint_solver="pgs"))
     _, _, tc = dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(constraint_solver="exact"))
-    assert tc.solver == 1 and tc.solver_iterations == 0
+    assert tc.solver == 1 and tc.solver_iterations == 0 and tc.solver_refine == 0
+
+
+def test_solver_refine_option(dp):
+    """TaskConfig.solver_refine reaches ps_task_cfg.solver_refine (0 none, 1 coupled substeps,
+    2 every substep); other values raise (ps_create rejects them too)."""
+    for r in (0, 1, 2):
+        _, _, tc = dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(solver_refine=r))
+        assert tc.solver_refine == r
+    with pytest.raises(ValueError, match="solver_refine"):
+        dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(solver_refine=3))
 
 
 def test_newton_converges_and_no_row_cap(dp, ref):

@@ -29,7 +29,7 @@ def rows(d, pattern):
 # its kernel instantiation: pianosim_kernel<true> (box / hull colliders) or <false> (all-capsule
 # hand); bench.py's line also times the other sets (its legs), which must not mix in
 HAND = __import__("os").environ.get("PIANOSIM_HAND", "hull")
-KNAME = "pianosim_kernel<false>" if HAND == "authored" else "pianosim_kernel<true>"
+KNAME = "pianosim_kernel<false" if HAND == "authored" else "pianosim_kernel<true"  # <XG, waves per SIMD>
 
 
 def counter(d, name):

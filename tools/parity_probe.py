@@ -30,6 +30,7 @@ from helpers import DATA, perturbed, song  # noqa: E402
 import test_gpu_solver as ts  # noqa: E402
 
 KEYS = ts.KEYS
+REFINE = int(os.environ.get("PIANOSIM_REFINE", "0"))  # the GPU env's TaskConfig.solver_refine
 
 
 def _stats(e, floor=None):
@@ -46,25 +47,25 @@ def _stats(e, floor=None):
 
 
 def case_bench():
-    md, g, o = ts._pair(dp, ref, "crossing_field", 64)
+    md, g, o = ts._pair(dp, ref, "crossing_field", 64, solver_refine=REFINE)
     o2 = ref.OracleEnv(*dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True),
                                         canonical_actions=False), 64)
     return _stats(*ts._teacher_forced(md, g, o, o2, 16, np.random.RandomState(21)))
 
 
 def case_coupled():
-    n, e, f = ts._replay(dp, ref, lambda st: st[:, 4] >= 10)
+    n, e, f = ts._replay(dp, ref, lambda st: st[:, 4] >= 10, solver_refine=REFINE)
     return _stats(e, f)
 
 
 def case_heavy():
-    n, e, f = ts._replay(dp, ref, lambda st: st[:, 3] > 40)
+    n, e, f = ts._replay(dp, ref, lambda st: st[:, 3] > 40, solver_refine=REFINE)
     return _stats(e, f)
 
 
 def _drift_tf(kind, steps=200, n=8):
     """tests/test_gpu_drift.py's teacher-forced part (env i starts 20 i actions into the trace)."""
-    task = dp.TaskConfig()
+    task = dp.TaskConfig(solver_refine=REFINE)
     seq = song(dp, "twinkle")
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
@@ -104,7 +105,7 @@ def case_random():
 def case_guren():
     N = 4096
     seq = song(dp, "guren")
-    task = dp.TaskConfig(trim_silence=True)
+    task = dp.TaskConfig(trim_silence=True, solver_refine=REFINE)
     g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", canonical_actions=False)
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     lo, hi = (torch.tensor(x, device="cuda:0", dtype=torch.float32) for x in dp.model.action_spec(md))
