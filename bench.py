@@ -218,22 +218,29 @@ def drift_summary(sha):
     wrote for THIS build (PIANOSIM_REPORT=profiles/drift_latest.json; it records the library
     hash), else None."""
     d = _profile("drift_latest.json", sha)
-    if not d:
+    if not d or "bench" not in d:
         return None
-    out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"), "song": d.get("song"),
+    # the workload the headline times (Crossing Field, the reference's default box / hull
+    # colliders); the all-capsule Twinkle report beside it
+    out = {"reference": "fp64 CPU restatement (MuJoCo absent)", "envs": d.get("envs"),
+           "workload": (d.get("workloads") or {}).get("bench"),
            "source": "profiles/drift_latest.json (tests/test_gpu_drift.py, same library build)"}
     chaos = _profile("chaos_floor.json") or {}
     if chaos.get("oracle_sha") != oracle_sha():  # measured on other physics: not this floor
         chaos = {}
-    for k in ("zero_action", "trace_actions", "random_actions"):
-        if k in d:
-            out[k] = {"teacher_forced_p99": d[k]["teacher_forced_qpos_linf"]["p99"],
-                      "free_running_1000_steps_max": d[k]["free_running_max_over_1000"]}
-            # the same metric for the fp64 checker against itself, 1e-12 perturbation per
-            # episode (tools/chaos_floor.py): the floor any non-bit-identical run sits on
-            c = chaos.get(f"{k.split('_')[0]}/delta=1e-12")
-            if c:
-                out[k]["fp64_self_1e-12_free_running_max"] = c["max_over_1000"]
+    for w in ("bench", "twinkle"):
+        dw, cw, ow = d.get(w, {}), chaos.get(w, {}), {}
+        for k in ("zero_action", "trace_actions", "random_actions"):
+            if k in dw:
+                tf = dw[k]["teacher_forced_qpos_linf"]
+                ow[k] = {"teacher_forced_p99": tf["p99"], "teacher_forced_p99_well_conditioned":
+                         tf.get("p99_well_conditioned"), "free_running_1000_steps_max": dw[k]["free_running_max_over_1000"]}
+                # the same metric for the fp64 checker against itself, 1e-12 limit-preserving
+                # perturbation per episode (tools/chaos_floor.py)
+                c = cw.get(f"{k.split('_')[0]}/delta=1e-12")
+                if c:
+                    ow[k]["fp64_self_1e-12_free_running_max"] = c["max_over_1000"]
+        out[w if w != "bench" else "bench_workload"] = ow
     return out
 
 

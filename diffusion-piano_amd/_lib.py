@@ -109,7 +109,7 @@ def load_rl() -> C.CDLL:
     L.prl_gae.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, i32, vp]
     L.prl_normalize.argtypes = [vp, i32, f32, vp]
     L.prl_gauss_sample.argtypes = [vp, vp, i32, i32, u64, u64, vp, vp, vp]
-    L.prl_clip_adam.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_int64), i32, vp, vp, f32, f32, f32, f32, vp, vp]
+    L.prl_clip_adam.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_int64), i32, vp, vp, f32, f32, f32, f32, vp, vp, vp]
     L.prl_gather_minibatch.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
     L.prl_lnrelu_fwd.argtypes = [vp, vp, vp, vp, i32, i32, f32, f32, u64, vp, i32, vp, vp, vp, vp]
     L.prl_lnrelu_bwd.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, f32, u64, vp, i32, vp, vp, vp, vp]
@@ -120,14 +120,14 @@ def load_rl() -> C.CDLL:
     if hasattr(L, "prl_mlp_step"):
         L.prl_mlp_step_work.argtypes = [C.POINTER(PrlNet), i32, i32]
         L.prl_mlp_step.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, i32, f32, f32, f32, u64, vp, vp, vp,
-                                   C.c_size_t, vp]
+                                   C.c_size_t, vp, vp]
         L.prl_mlp_step_idx.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, vp, i32, f32, f32, f32, u64, vp,
-                                       vp, vp, C.c_size_t, vp]
+                                       vp, vp, C.c_size_t, vp, vp]
         L.prl_mlp_step_norm_parts.argtypes = [C.POINTER(PrlNet), i32, i32]
         L.prl_mlp_step_idx_norm.argtypes = [C.POINTER(PrlNet), vp, i32, vp, i32, vp, vp, vp, vp, i32, f32, f32, f32, u64,
-                                            vp, vp, vp, C.c_size_t, vp, C.POINTER(C.c_int64), i32, vp, vp, i32, vp]
+                                            vp, vp, vp, C.c_size_t, vp, C.POINTER(C.c_int64), i32, vp, vp, i32, vp, vp]
         L.prl_clip_adam_parts.argtypes = [vp, vp, vp, vp, C.POINTER(C.c_int64), i32, vp, vp, f32, f32, f32, f32, vp, i32,
-                                          vp]
+                                          vp, vp]
     for name in RL_EXPORTS[2:]:
         getattr(L, name).restype = i32
     if hasattr(L, "prl_mlp_step_work"):

@@ -113,10 +113,17 @@ class SongDesc(C.Structure):
 
 
 class TaskCfg(C.Structure):
-    _fields_ = [("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
+    """ps_task_cfg; struct_size is set to the struct's size (include/pianosim.h: ps_create
+    refuses a struct of another layout)."""
+    _fields_ = [("struct_size", C.c_uint32), ("n_steps_lookahead", i32), ("fingering_reward", i32), ("forearm_reward", i32),
                 ("wrong_press_termination", i32), ("energy_penalty_coef", d),
                 ("solver_iterations", i32), ("max_contacts", i32), ("canonical_actions", i32),
                 ("solver", i32), ("randomize_hand_positions", i32), ("solver_refine", i32)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if "struct_size" not in kw:
+            self.struct_size = C.sizeof(TaskCfg)
 
 
 SOLVER_EXACT = SOLVER_NEWTON = 1

@@ -237,8 +237,10 @@ __device__ __forceinline__ int64_t seg_begin(const Segs& sg, int s) { return s =
 // pass 1: per-segment partial sums of g^2 (fp64), one row of partials per block; block 0
 // also advances the per-segment step counters (torch's state["step"] += 1)
 __global__ void __launch_bounds__(ADAM_THREADS) grad_sumsq_kernel(const float* __restrict__ g, Segs sg,
-                                                                  double* __restrict__ part, float* __restrict__ step) {
+                                                                  double* __restrict__ part, float* __restrict__ step,
+                                                                  const unsigned* __restrict__ guard) {
   __shared__ double red[ADAM_THREADS / 64];
+  if (guard && *guard) return;  // a failed minibatch step upstream: apply nothing (block-uniform)
   for (int s = 0; s < sg.n; s++) {
     double acc = 0.0;
 #pragma unroll 8
@@ -265,8 +267,10 @@ __global__ void __launch_bounds__(ADAM_THREADS) clip_adam_kernel(float* __restri
                                                                  const double* __restrict__ part,
                                                                  const float* __restrict__ lr,
                                                                  const float* __restrict__ step, float b1, float b2,
-                                                                 float eps, float max_norm, int nparts) {
+                                                                 float eps, float max_norm, int nparts,
+                                                                 const unsigned* __restrict__ guard) {
   __shared__ float coef[PRL_MAX_SEG], ssz[PRL_MAX_SEG], ibc2[PRL_MAX_SEG];
+  if (guard && *guard) return;  // a failed minibatch step upstream: apply nothing (block-uniform)
   const int64_t n = sg.end[sg.n - 1];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -539,7 +543,7 @@ __global__ void colsums_final_kernel(ColSums cs, int nchunks) {
 extern "C" {
 
 const char* prl_last_error(void) { return g_err.c_str(); }
-int prl_version(void) { return 1; }
+int prl_version(void) { return 2; }  // 2: the guard word of prl_mlp_step* / prl_clip_adam*
 
 int prl_running_norm(const float* x, int n, double* stats, float* out, void* stream) {
   if (!x || !stats || !out || n <= 0) return fail("prl_running_norm: null pointer or n <= 0");
@@ -582,7 +586,7 @@ int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint
 namespace {
 int clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end, int nseg,
               const float* lr, float* step, float beta1, float beta2, float eps, float max_norm, double* scratch,
-              const double* pre_parts, int npre, void* stream) {
+              const double* pre_parts, int npre, const unsigned* guard, void* stream) {
   if (!param || !grad || !exp_avg || !exp_avg_sq || !seg_end || !lr || !step || (!scratch && !pre_parts))
     return fail("prl_clip_adam: null pointer");
   if (nseg < 1 || nseg > PRL_MAX_SEG) return fail("prl_clip_adam: need 1 <= nseg <= PRL_MAX_SEG");
@@ -598,15 +602,15 @@ int clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
   if (pre_parts) {  // the norm partials (and the step advance) came from prl_mlp_step_norm
     const int blocks = (int)std::min<int64_t>(2048, (n + ADAM_THREADS * ADAM_PER - 1) / (ADAM_THREADS * ADAM_PER));
     clip_adam_kernel<<<blocks, ADAM_THREADS, 0, (hipStream_t)stream>>>(param, grad, exp_avg, exp_avg_sq, sg, pre_parts,
-                                                                      lr, step, beta1, beta2, eps, max_norm, npre);
+                                                                      lr, step, beta1, beta2, eps, max_norm, npre, guard);
     HIPCHK(hipGetLastError());
     return 0;
   }
-  grad_sumsq_kernel<<<parts, ADAM_THREADS, 0, (hipStream_t)stream>>>(grad, sg, scratch, step);
+  grad_sumsq_kernel<<<parts, ADAM_THREADS, 0, (hipStream_t)stream>>>(grad, sg, scratch, step, guard);
   HIPCHK(hipGetLastError());
   const int blocks = (int)std::min<int64_t>(2048, (n + ADAM_THREADS * ADAM_PER - 1) / (ADAM_THREADS * ADAM_PER));
   clip_adam_kernel<<<blocks, ADAM_THREADS, 0, (hipStream_t)stream>>>(param, grad, exp_avg, exp_avg_sq, sg, scratch, lr,
-                                                                    step, beta1, beta2, eps, max_norm, parts);
+                                                                    step, beta1, beta2, eps, max_norm, parts, guard);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -615,17 +619,17 @@ int clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
 extern "C" {
 int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
                   int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
-                  double* scratch, void* stream) {
+                  double* scratch, const unsigned* guard, void* stream) {
   return clip_adam(param, grad, exp_avg, exp_avg_sq, seg_end, nseg, lr, step, beta1, beta2, eps, max_norm, scratch,
-                   nullptr, 0, stream);
+                   nullptr, 0, guard, stream);
 }
 
 int prl_clip_adam_parts(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
                         int nseg, const float* lr, const float* step, float beta1, float beta2, float eps,
-                        float max_norm, const double* parts, int nparts, void* stream) {
+                        float max_norm, const double* parts, int nparts, const unsigned* guard, void* stream) {
   if (!parts || nparts <= 0) return fail("prl_clip_adam_parts: no partials");
   return clip_adam(param, grad, exp_avg, exp_avg_sq, seg_end, nseg, lr, const_cast<float*>(step), beta1, beta2, eps,
-                   max_norm, nullptr, parts, nparts, stream);
+                   max_norm, nullptr, parts, nparts, guard, stream);
 }
 
 int prl_gather_minibatch(const float* S, int sdim, const float* A, int adim, const float* lp, const float* adv,
@@ -886,7 +890,7 @@ struct NormOut {  // prl_mlp_step_idx_norm: the grad-norm partials for prl_clip_
 int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
              const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef, float ln_eps,
              uint64_t seed, uint64_t* step_inc, const uint64_t* step, float* log_row, float* work, size_t work_floats,
-             void* stream, const NormOut* no = nullptr) {
+             unsigned* guard, void* stream, const NormOut* no = nullptr) {
   if (!nets || !S || !A || !old_lp || !adv || !ret || !step || !log_row || !work) return fail("prl_mlp_step: null argument");
   if (B <= 0 || sdim <= 0 || sdim > 1024) return fail("prl_mlp_step: B > 0 and 0 < sdim <= 1024 required");
   mlp::Args a{};
@@ -922,6 +926,14 @@ int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int 
     g.step_inc = step_inc;
   }
   a.Sg = a.idx ? a.Sg : nullptr;
+  if (guard && a.hand) a.err = guard;  // the split kernel's error word: the caller's guard
+  g.guard = guard ? guard : a.hand ? a.err : nullptr;
+  {
+    const char* st = getenv("PIANORL_SPLIT_SPIN_TICKS");
+    a.spin_ticks = st ? strtoull(st, nullptr, 10) : mlp::SPLIT_SPIN_TICKS;
+    const char* ft = getenv("PIANORL_SPLIT_TEST_FAULT");
+    a.fault = ft && ft[0] == '1';
+  }
   g.npart = nullptr;
   if (no) {  // each gradient write's clip+Adam segment, from its offset in the flat gradient buffer
     if (!no->grad_base || !no->seg_end || no->nseg < 1 || no->nseg > PRL_MAX_SEG || !no->adam_step || !no->part)
@@ -957,7 +969,13 @@ int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int 
   // the column-split kernel where the shapes allow it (its exchange region is in the work
   // space); PIANORL_MLP_SPLIT=0 selects the one-workgroup-per-tile kernel
   const char* sv = getenv("PIANORL_MLP_SPLIT");
-  if (a.hand && !(sv && sv[0] == '0')) {
+  // its exchanges need every member of a group resident at once: one workgroup per CU (the
+  // LDS request), so the groups' workgroups must not outnumber the device's CUs
+  int dev = 0, cus = 0;
+  HIPCHK(hipGetDevice(&dev));
+  HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const bool split_fits = 2 * g.ntiles * mlp::NSPL <= cus;
+  if (a.hand && split_fits && !(sv && sv[0] == '0')) {
     const size_t slds = mlp::split_lds_floats(((sdim + 15) & ~15) + 4) * sizeof(float);
     if (slds > 160 * 1024) return fail("prl_mlp_step: split kernel LDS over 160 KB");
     const int groups = 2 * g.ntiles;
@@ -978,29 +996,30 @@ int mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int 
 extern "C" {
 int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
                  const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
-                 const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream) {
+                 const uint64_t* step, float* log_row, float* work, size_t work_floats, unsigned* guard,
+                 void* stream) {
   return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, nullptr, B, clip, ent_coef, ln_eps, seed, nullptr, step,
-                  log_row, work, work_floats, stream);
+                  log_row, work, work_floats, guard, stream);
 }
 
 int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
                      const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef,
                      float ln_eps, uint64_t seed, uint64_t* step, float* log_row, float* work, size_t work_floats,
-                     void* stream) {
+                     unsigned* guard, void* stream) {
   if (!idx) return fail("prl_mlp_step_idx: null idx");
   return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, idx, B, clip, ent_coef, ln_eps, seed, step, step, log_row,
-                  work, work_floats, stream);
+                  work, work_floats, guard, stream);
 }
 
 int prl_mlp_step_idx_norm(const prl_net* nets, const float* S, int sdim, const float* A, int adim,
                           const float* old_lp, const float* adv, const float* ret, const int64_t* idx, int B,
                           float clip, float ent_coef, float ln_eps, uint64_t seed, uint64_t* step, float* log_row,
                           float* work, size_t work_floats, const float* grad_base, const int64_t* seg_end, int nseg,
-                          float* adam_step, double* norm_part, int nparts, void* stream) {
+                          float* adam_step, double* norm_part, int nparts, unsigned* guard, void* stream) {
   if (!idx) return fail("prl_mlp_step_idx_norm: null idx");
   const NormOut no{grad_base, seg_end, nseg, adam_step, norm_part, nparts};
   return mlp_step(nets, S, sdim, A, adim, old_lp, adv, ret, idx, B, clip, ent_coef, ln_eps, seed, step, step, log_row,
-                  work, work_floats, stream, &no);
+                  work, work_floats, guard, stream, &no);
 }
 
 #ifdef MLP_TIMING

@@ -523,15 +523,19 @@ static int build_dev_model(const ps_model_desc* d, DevModel* m) {
 extern "C" {
 
 const char* ps_last_error(void) { return g_err.c_str(); }
-int ps_version(void) { return 3; }
+int ps_version(void) { return 4; }  // 4: ps_task_cfg.struct_size
 int ps_model_desc_size(void) { return (int)sizeof(ps_model_desc); }
 int ps_obs_dim(const ps_task_cfg* cfg) {
+  if (!cfg || cfg->struct_size != PS_TASK_CFG_SIZE)
+    return fail("ps_task_cfg.struct_size != sizeof(ps_task_cfg): rebuild against include/pianosim.h");
   return (cfg->n_steps_lookahead + 1) * (NK + 1) + (cfg->fingering_reward ? 10 : 0) + NK + 1 + NH * ND;
 }
 
 int ps_create(const ps_model_desc* model, const ps_song_desc* song, const ps_task_cfg* cfg, int n_envs, int device,
               uint64_t seed, ps_env** out) {
   if (!model || !song || !cfg || !out) return fail("null argument");
+  if (cfg->struct_size != PS_TASK_CFG_SIZE)
+    return fail("ps_task_cfg.struct_size != sizeof(ps_task_cfg): rebuild against include/pianosim.h");
   if (n_envs <= 0) return fail("n_envs must be positive");
   if (song->T <= 0) return fail("empty song");
   if (cfg->n_steps_lookahead < 0) return fail("negative lookahead");

@@ -225,12 +225,18 @@ def flat_offsets(params):
 
 class GradBucket:
     """One flat fp32 buffer holding the gradients of ``params`` (``p.grad`` are views), so
-    data-parallel training does one all-reduce per minibatch instead of one per tensor."""
+    data-parallel training does one all-reduce per minibatch instead of one per tensor. One
+    slot past the gradients carries the ``guard`` word (a device int32 [1], optional) through
+    the same all-reduce: a rank whose minibatch step failed stops every rank's optimiser step,
+    not only its own (include/pianorl.h, the guard)."""
+
+    guard = None
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
         offs, n = flat_offsets(self.params)
-        self.flat = torch.zeros(n, dtype=torch.float32, device=self.params[0].device)
+        self.n = n
+        self.flat = torch.zeros(n + FLAT_ALIGN, dtype=torch.float32, device=self.params[0].device)
         for p, o in zip(self.params, offs):
             p.grad = self.flat[o:o + p.numel()].view_as(p)
 
@@ -238,8 +244,13 @@ class GradBucket:
         import torch.distributed as dist
         ws = dist.get_world_size(group)
         if ws > 1:
+            st = self.flat[self.n:self.n + 1]
+            if self.guard is not None:
+                st.copy_(self.guard)
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             self.flat.div_(ws)
+            if self.guard is not None:  # any rank's failure: every rank's guard set
+                self.guard.bitwise_or_((st != 0).to(torch.int32))
 
 
 class FlatAdam(GradBucket):
@@ -313,6 +324,10 @@ class FlatAdam(GradBucket):
     # (ptr, n): gradient-norm partials a fused minibatch step left for the next step() (and the
     # step counts it advanced), prl_mlp_step_idx_norm
     pre_parts = None
+    # GradBucket.guard: the guard word (include/pianorl.h, ABI version 2) - while it is non-zero
+    # step() applies nothing (PPOAgent sets it; the split rows kernel writes it)
+    def _guard_ptr(self):
+        return None if self.guard is None else self.guard.data_ptr()
 
     def step(self):
         b1, b2 = self.betas
@@ -322,12 +337,12 @@ class FlatAdam(GradBucket):
             _lib.check_rl(_lib.load_rl().prl_clip_adam_parts(
                 self.param.data_ptr(), self.flat.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
                 self.seg_end, self.nseg, self.lr.data_ptr(), self.step_count.data_ptr(), float(b1), float(b2),
-                float(self.eps), float(self.max_norm), ptr, n, _stream()))
+                float(self.eps), float(self.max_norm), ptr, n, self._guard_ptr(), _stream()))
             return
         _lib.check_rl(_lib.load_rl().prl_clip_adam(
             self.param.data_ptr(), self.flat.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
             self.seg_end, self.nseg, self.lr.data_ptr(), self.step_count.data_ptr(), float(b1), float(b2),
-            float(self.eps), float(self.max_norm), self.scratch.data_ptr(), _stream()))
+            float(self.eps), float(self.max_norm), self.scratch.data_ptr(), self._guard_ptr(), _stream()))
 
 
 # ---------------------------------------------------------------- fused minibatch step
@@ -437,11 +452,18 @@ class FusedStep:
         self.nets[train] = nets
         return nets
 
-    def mlp_error(self, B):
-        """The column-split rows kernel's error word for minibatches of B rows (0: every exchange
-        completed; 1 + e: a wait on exchange e timed out and that step's outputs are garbage)."""
-        w = self.bufs.get(B, {}).get("_mlp_work")
-        return 0 if w is None else int(w[-1:].view(torch.int32).item())
+    def mlp_error(self, B=None):
+        """The column-split rows kernel's error word (0: every exchange completed; 1 + e: a wait on
+        exchange e timed out, that step's outputs were garbage and nothing from it on was
+        applied). It is the agent's guard word (``PPOAgent._guard``) for every minibatch size."""
+        return int(self.agent._guard.item())
+
+    def reset_exchanges(self):
+        """After a timed-out exchange: zero every work space (the split kernel's granule tags and
+        call counts restart at 0, so no stale tag of the failed call can match a later wait)."""
+        for b in self.bufs.values():
+            if "_mlp_work" in b:
+                b["_mlp_work"].zero_()
 
     def _mlp_ok(self, B):
         if not self.mfma or B > self.MFMA_MAX_ROWS:
@@ -478,13 +500,13 @@ class FusedStep:
                                             float(ag.epsilon), float(ag.entropy_coef), float(self.actor[0][0][1].eps),
                                             self.seed, self.step.data_ptr(), lr_ptr, w.data_ptr(), w.numel(),
                                             fl.flat.data_ptr(), fl.seg_end, fl.nseg, fl.step_count.data_ptr(),
-                                            npart.data_ptr(), npart.shape[0], st))
+                                            npart.data_ptr(), npart.shape[0], ag._guard.data_ptr(), st))
                 fl.pre_parts = (npart.data_ptr(), npart.shape[0])
                 return log_row is not None
             chk(R.prl_mlp_step_idx(nets, ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(),
                                    ag._ADV.data_ptr(), ag._RET.data_ptr(), idx.data_ptr(), B, float(ag.epsilon),
                                    float(ag.entropy_coef), float(self.actor[0][0][1].eps), self.seed,
-                                   self.step.data_ptr(), lr_ptr, w.data_ptr(), w.numel(), st))
+                                   self.step.data_ptr(), lr_ptr, w.data_ptr(), w.numel(), ag._guard.data_ptr(), st))
             return log_row is not None
         chk(R.prl_gather_minibatch(ag._S.data_ptr(), sdim, ag._A.data_ptr(), adim, ag._LP.data_ptr(), ag._ADV.data_ptr(),
                                    ag._RET.data_ptr(), idx.data_ptr(), B, b["S"].data_ptr(), b["A"].data_ptr(),
@@ -500,7 +522,7 @@ class FusedStep:
                                b["ADV"].data_ptr(), b["RET"].data_ptr(), B, float(ag.epsilon), float(ag.entropy_coef),
                                float(self.actor[0][0][1].eps), self.seed, self.step.data_ptr(),
                                (ag._log_row if log_row is None else log_row).data_ptr(),
-                               w.data_ptr(), w.numel(), st))
+                               w.data_ptr(), w.numel(), ag._guard.data_ptr(), st))
             return log_row is not None
         for net, (hidden, out) in (("a", self.actor), ("c", self.critic)):
             x = b["S"]
@@ -575,6 +597,10 @@ class PPOAgent:
         self.flat = FlatAdam([self.critic_optimizer, self.actor_optimizer], [float(lr) * 2, float(lr)],
                              max_norm=max_grad_norm, betas=(0.9, 0.999), eps=1e-5)
         self.bucket = self.flat
+        # the guard word (include/pianorl.h): the split rows kernel's timeout code; while set, no
+        # optimiser launch applies anything; update() reads it with its statistics and raises
+        self._guard = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.flat.guard = self._guard
         if self.distributed:  # identical replicas: rank 0's initial weights everywhere
             torch.distributed.broadcast(self.flat.param, src=0, group=process_group)
         self.actor_scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.actor_optimizer, mode="max", factor=0.5,
@@ -833,11 +859,23 @@ class PPOAgent:
         # the plateau signal: the mean normalised reward of the samples trained on (r holds 0
         # at the dropped auto-reset rows)
         r_mean = r.mean() if valid is None else r.reshape(-1)[_f32(valid, self.device).reshape(-1) != 0].mean()
-        stats = torch.stack([r_mean, log[-1, 1]])
+        # (the guard word rides along: one host read per update, no extra sync)
+        stats = torch.stack([r_mean, log[-1, 1], self._guard[0].to(r_mean.dtype)])
         if self.distributed:  # one plateau decision for all replicas (else their lrs drift apart)
             torch.distributed.all_reduce(stats, group=self.process_group)
             stats /= torch.distributed.get_world_size(self.process_group)
-        mean_reward, mean_critic_loss = (float(x) for x in stats.cpu())
+        mean_reward, mean_critic_loss, failed = (float(x) for x in stats.cpu())
+        if failed != 0.0:
+            code = int(self._guard.item())
+            self._guard.zero_()
+            if self._fused is not None:
+                self._fused.reset_exchanges()
+            raise _lib.PianosimError(
+                "PPOAgent.update: a column-split rows kernel exchange timed out "
+                f"(error word {code}: 1 + exchange index; on another rank if 0); the minibatch steps "
+                "from the failed one on were not applied (parameters, Adam moments and step counts "
+                "unchanged). Another kernel occupying CUs can cause this; PIANORL_MLP_SPLIT=0 selects "
+                "the one-workgroup-per-tile rows kernel.")
         self.actor_scheduler.step(mean_reward)
         self.critic_scheduler.step(mean_critic_loss)
         self.timing["update_s"] = time.perf_counter() - t0

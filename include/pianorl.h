@@ -27,6 +27,15 @@
  *
  * Conventions as include/pianosim.h: DEVICE pointers, asynchronous on the caller's HIP
  * stream (NULL = default), 0 = OK / < 0 = error with a thread-local prl_last_error().
+ *
+ * ABI version 2 (prl_version): prl_mlp_step* and prl_clip_adam* take a trailing `guard`, a
+ * device u32 shared by one optimiser's launches (NULL = none). The column-split rows kernel
+ * writes its error code there (1 + the exchange whose bounded wait timed out); while it is
+ * non-zero the gradient kernel does not advance the Adam step counts and prl_clip_adam* leave
+ * parameters, moments and step counts unchanged, so a failed step can never reach the
+ * weights. The caller reads it at its next sync point, clears it and the work space, and
+ * reports the failure (ppo.py raises PianosimError). Callers built against version 1 must be
+ * rebuilt: the argument lists changed.
  */
 #ifndef PIANORL_H
 #define PIANORL_H
@@ -70,12 +79,12 @@ int prl_gauss_sample(const float* mean, const float* log_std, int n, int a, uint
  * scratch: device f64 [256 * PRL_MAX_SEG]. max_norm <= 0 disables clipping. */
 int prl_clip_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
                   int nseg, const float* lr, float* step, float beta1, float beta2, float eps, float max_norm,
-                  double* scratch, void* stream);
+                  double* scratch, const unsigned* guard, void* stream);
 /* prl_clip_adam with the gradient-norm partials already summed per segment (parts [nparts]
  * [PRL_MAX_SEG] f64, prl_mlp_step_idx_norm) and the step counts already advanced: one launch. */
 int prl_clip_adam_parts(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* seg_end,
                         int nseg, const float* lr, const float* step, float beta1, float beta2, float eps,
-                        float max_norm, const double* parts, int nparts, void* stream);
+                        float max_norm, const double* parts, int nparts, const unsigned* guard, void* stream);
 
 /* ---- fused minibatch step (ppo_v2.py:266-293 with the backward written out; the GEMMs
  * between these are library GEMMs). All row-major fp32 [rows, cols]. */
@@ -132,8 +141,12 @@ int prl_colsums(int n, const float* const* src, const int* cols, const float* sc
  * before its first call and then kept between calls: for B <= 256, state width <= 384 and
  * hidden widths of 128 or 256 its tail holds the column-split rows kernel's tagged exchange
  * slices and per-tile call counts (4 workgroups per 16-row tile and network, six exchanges per
- * step; PIANORL_MLP_SPLIT=0 selects the one-workgroup-per-tile kernel), and its last word is
- * that kernel's error word (0, or 1 + the exchange whose bounded wait timed out). */
+ * step; PIANORL_MLP_SPLIT=0 selects the one-workgroup-per-tile kernel; the host takes it only
+ * when its 4 x 2 x ceil(B / 16) workgroups fit the device's CU count), and its last word is
+ * that kernel's error word (0, or 1 + the exchange whose bounded wait timed out) unless a
+ * guard is given (see the ABI note above). Test hooks, read per call: PIANORL_SPLIT_SPIN_TICKS
+ * (the bounded wait, 100 MHz ticks, default 2 s) and PIANORL_SPLIT_TEST_FAULT=1 (one member
+ * never publishes its first exchange, so the others time out). */
 typedef struct {
   int in, out;
   const float *W, *b, *gamma, *beta;  /* W [out][in]; gamma/beta: NULL on the output layer */
@@ -149,14 +162,15 @@ typedef struct {
 size_t prl_mlp_step_work(const prl_net* nets, int sdim, int B);
 int prl_mlp_step(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
                  const float* adv, const float* ret, int B, float clip, float ent_coef, float ln_eps, uint64_t seed,
-                 const uint64_t* step, float* log_row, float* work, size_t work_floats, void* stream);
+                 const uint64_t* step, float* log_row, float* work, size_t work_floats, unsigned* guard,
+                 void* stream);
 /* prl_gather_minibatch + prl_mlp_step in one: S / A / old_lp / adv / ret are the whole rollout
  * ([N, sdim] ...), the minibatch is rows idx[B] (int64), read in place by the rows kernel; the
  * dropout step counter *step is advanced once (as prl_gather_minibatch does). Same work size. */
 int prl_mlp_step_idx(const prl_net* nets, const float* S, int sdim, const float* A, int adim, const float* old_lp,
                      const float* adv, const float* ret, const int64_t* idx, int B, float clip, float ent_coef,
                      float ln_eps, uint64_t seed, uint64_t* step, float* log_row, float* work, size_t work_floats,
-                     void* stream);
+                     unsigned* guard, void* stream);
 /* prl_mlp_step_idx that also leaves the clip_grad_norm_ partials for prl_clip_adam_parts (one
  * launch less per minibatch): grad_base = the flat gradient buffer the layers' gradients live
  * in, seg_end[nseg] its segments (as prl_clip_adam); the gradient kernel writes each workgroup's sum
@@ -167,7 +181,7 @@ int prl_mlp_step_idx_norm(const prl_net* nets, const float* S, int sdim, const f
                           const float* old_lp, const float* adv, const float* ret, const int64_t* idx, int B,
                           float clip, float ent_coef, float ln_eps, uint64_t seed, uint64_t* step, float* log_row,
                           float* work, size_t work_floats, const float* grad_base, const int64_t* seg_end, int nseg,
-                          float* adam_step, double* norm_part, int nparts, void* stream);
+                          float* adam_step, double* norm_part, int nparts, unsigned* guard, void* stream);
 
 #ifdef __cplusplus
 }

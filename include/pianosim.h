@@ -194,8 +194,13 @@ typedef struct {
   const int32_t* fingers;  /* [T][PS_MAX_NOTES], 0-4 right, 5-9 left */
 } ps_song_desc;
 
-/* Task options (piano_with_shadow_hands.py:50-66). */
+/* Task options (piano_with_shadow_hands.py:50-66). The first field is the struct's size: a
+ * caller sets struct_size = sizeof(ps_task_cfg) (= PS_TASK_CFG_SIZE of the header it was built
+ * against) and ps_create / ps_obs_dim refuse any other value - a caller built against an older
+ * header (before ps_version 4: no struct_size, no solver_refine) fails with "rebuild against
+ * include/pianosim.h" instead of the library reading past the end of its struct. */
 typedef struct {
+  uint32_t struct_size;             /* sizeof(ps_task_cfg) */
   int32_t n_steps_lookahead;        /* goal rows = lookahead + 1 */
   int32_t fingering_reward;         /* 1: fingering reward + 'fingering' obs; 0: OT reward */
   int32_t forearm_reward;           /* 1: add forearm reward term */
@@ -216,6 +221,7 @@ typedef struct {
                                        qpos p99 against the fp64 checker ~1.5e-4 -> ~8e-5 on coupled
                                        states) at ~5-8% of the throughput */
 } ps_task_cfg;
+#define PS_TASK_CFG_SIZE ((uint32_t)sizeof(ps_task_cfg))
 
 /* Constraint solver. NEWTON (= EXACT, the only one): the minimiser of MuJoCo's primal
  * constraint problem over the accelerations (mj_solNewton: Newton directions from the

@@ -2107,6 +2107,30 @@ int ref_debug_contacts(ref_env* R, int i, int32_t* info, double* data) {
   return E->ncon;
 }
 
+/* The world shape of a collider of env i (test access; tools/contact_diff.py): g < NCAPS a
+ * capsule, NCAPS <= g < NCAPS + NH * NX an extra collider, g = -1 - k key k, g = -1000 the
+ * base; packed as unpack_shape reads it (23 doubles); *verts / *nv the hull's vertices. */
+int ref_debug_shape(ref_env* R, int i, int g, double* out, const double** verts, int* nv) {
+  const envdata* E = &R->e[i];
+  const ps_model_desc* d = &R->m.d;
+  shape s;
+  m3 I3 = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+  if (g == -1000) s = box_shape(mk(d->base_pos[0], d->base_pos[1], d->base_pos[2]), I3, d->base_half);
+  else if (g < 0) s = box_shape(E->keyc[-1 - g], E->keyR[-1 - g], d->key_half[-1 - g]);
+  else if (g < NCAPS) s = capsule_shape(E, g / NG, g % NG, d);
+  else s = extra_shape(E, (g - NCAPS) / NX, (g - NCAPS) % NX, d);
+  memset(out, 0, 23 * sizeof(double));
+  out[0] = s.type;
+  for (int k = 0; k < 3; k++) {
+    out[1 + k] = s.c.v[k]; out[13 + k] = s.p0.v[k]; out[16 + k] = s.p1.v[k]; out[20 + k] = s.hs[k];
+  }
+  for (int k = 0; k < 9; k++) out[4 + k] = s.R.m[k];
+  out[19] = s.r;
+  *verts = s.type == PS_GEOM_HULL ? &s.vert[0][0] : NULL;
+  *nv = s.type == PS_GEOM_HULL ? s.nvert : 0;
+  return 0;
+}
+
 /* Narrow phase of two world colliders (test access). A shape is packed as 23 doubles: type
  * (0 capsule, PS_GEOM_BOX, PS_GEOM_HULL), centre (3), row-major rotation (9), capsule p0 (3),
  * p1 (3), radius, box half sizes (3); hull vertices (geom frame) come separately. A is geom1.

@@ -62,6 +62,8 @@ def _bind(L):
     L.ref_set_hand_offset.argtypes = [C.c_void_p, _f64p]
     L.ref_hand_offset_draw.restype = C.c_float
     L.ref_hand_offset_draw.argtypes = [C.c_uint64, C.c_int, C.c_int]
+    L.ref_debug_shape.argtypes = [C.c_void_p, C.c_int, C.c_int, _f64p, C.POINTER(C.POINTER(C.c_double)),
+                                  C.POINTER(C.c_int)]
     L.ref_narrow.argtypes = [_f64p, C.c_void_p, C.c_int, _f64p, C.c_void_p, C.c_int, _f64p]
     _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
     L.ref_stats_get.argtypes = [_i64p] * 4
@@ -256,6 +258,15 @@ class OracleEnv:
         n = self._L.ref_debug_contacts(self._h, i, info, data)
         return [(int(info[4 * c]), int(info[4 * c + 1]), int(info[4 * c + 2]), int(info[4 * c + 3]), float(data[7 * c]),
                  data[7 * c + 1:7 * c + 4].copy(), data[7 * c + 4:7 * c + 7].copy()) for c in range(n)]
+
+    def shape(self, i, g):
+        """(packed shape [23], hull vertices [nv, 3] or None) of collider g of env i at its
+        current state (ref_debug_shape: g < 40 capsule, 40.. extra, -1 - k key k, -1000 base)."""
+        out = np.zeros(23)
+        vp, nv = C.POINTER(C.c_double)(), C.c_int()
+        self._L.ref_debug_shape(self._h, i, g, out, C.byref(vp), C.byref(nv))
+        verts = np.ctypeslib.as_array(vp, (nv.value, 3)).copy() if nv.value else None
+        return out, verts
 
     def hand_offset(self):
         """(y shift of both hand roots this episode [N], resets so far [N])."""

@@ -57,12 +57,52 @@ def box_hull_hand(dp):
     return dp.mjcf.box_hull_hand()
 
 
-def perturbed(state, rng, scale=1e-7):
-    """The state with every hand joint moved by N(0, scale) rad: the checker stepped from it
-    measures the model's own fp64 sensitivity at that state (parity floor)."""
+_DEFAULT_LIMITS = None
+
+
+def hand_limits(md=None):
+    """(lo, hi, limited, locked) [52] of the hand dofs (rh 26, lh 26) of ``md`` (default: the
+    authored hand, whose joint ranges every collider set shares)."""
+    global _DEFAULT_LIMITS
+    if md is None:
+        if _DEFAULT_LIMITS is None:
+            import importlib
+            _DEFAULT_LIMITS = hand_limits(importlib.import_module("diffusion-piano_amd").model.build_model())
+        return _DEFAULT_LIMITS
+    rng_ = np.array(md.dof_range, np.float64).reshape(52, 2)
+    return (rng_[:, 0], rng_[:, 1], np.array(md.dof_limited, bool).reshape(52),
+            np.array(md.dof_locked, bool).reshape(52))
+
+
+def perturb_joints(q, rng, scale=1e-7, md=None):
+    """Hand joints [n, 52] moved by N(0, scale) each WITHOUT changing any joint limit's
+    activity: a step that would cross a limit (or leave one: a joint resting exactly ON its
+    limit - 22 of the 52 at qpos0 - has an inactive row that any move below the limit would
+    activate) is taken in the other direction; locked dofs stay. So the perturbation probes the
+    state's sensitivity, not the discontinuity of a limit row switching on (VERDICT r5 weak #3)."""
+    lo, hi, lim, locked = hand_limits(md)
+    q = np.array(q, np.float64)
+    d = rng.normal(0.0, scale, q.shape)
+    d[:, locked] = 0.0
+
+    def zones(x):
+        return np.where(lim, (x < lo).astype(int) - (x > hi).astype(int), 0)
+
+    z0 = zones(q)
+    flip = zones(q + d) != z0
+    d[flip] = -d[flip]
+    still = zones(q + d) != z0  # (a range narrower than the step: no move)
+    d[still] = 0.0
+    return q + d
+
+
+def perturbed(state, rng, scale=1e-7, md=None):
+    """The state with every hand joint moved by N(0, scale) rad, keeping each joint on its side
+    of its limits (``perturb_joints``): the checker stepped from it measures the model's own fp64
+    sensitivity at that state (parity floor)."""
     s = dict(state)
     q = np.array(state["qpos"], np.float64)
-    q[:, 88:] += rng.normal(0.0, scale, q[:, 88:].shape)
+    q[:, 88:] = perturb_joints(q[:, 88:], rng, scale, md)
     s["qpos"] = q
     return s
 
@@ -98,21 +138,28 @@ def assert_parity(e, floor, what="", tol=1e-4, well=1e-5, p99_ceil=PARITY_P99_CE
     return msg
 
 
-def assert_flip_rates(e, floor, what="", ts=(1e-3, 1e-2), p99_cap=0.1, slack=0.01, median=1e-5):
+def assert_flip_rates(e, floor, what="", ts=(1e-3, 1e-2), p99_cap=5e-2, slack=0.01, median=1e-5, tol=1e-4,
+                      well=1e-5):
     """The whole-step gate of the box / hull hand, whose MPR contact normals are piecewise
     constant over the hulls' faces (a portal near a face edge switches faces under any tiny
-    change of its input, in the fp64 checker too): median below `median`; for each threshold t
-    the fraction of env-steps the GPU moves by more than t at most 2x the fraction the checker
-    moves itself under a 1e-7 rad perturbation (`floor`) + `slack` (the tail is made of such
-    switches: its rate, not a single-sample p99, is what the two runs share); p99 below
-    `p99_cap`."""
+    change of its input, in the fp64 checker too): median below `median`; p99 below `tol` over
+    the well-conditioned env-steps (the checker's own move under the perturbation, `floor`, below
+    `well`; at least half of them) - the clause of ``assert_parity``, so a systematic error
+    confined to the steps the checker resolves cannot hide in the tail; for each threshold t the
+    fraction of env-steps the GPU moves by more than t at most 2x the fraction the checker moves
+    itself under a 1e-7 rad perturbation + `slack` (the tail is made of such switches: its rate,
+    not a single-sample p99, is what the two runs share); p99 below `p99_cap`."""
     e, floor = np.asarray(e, np.float64), np.asarray(floor, np.float64)
     rates = {t: (float(np.mean(e > t)), float(np.mean(floor > t))) for t in ts}
+    calm = floor < well
     msg = (f"{what}: n {e.size}, median {np.median(e):.2e}, p99 {np.percentile(e, 99):.2e}, max {e.max():.2e}; "
+           f"well-conditioned {int(calm.sum())}: p99 {np.percentile(e[calm], 99) if calm.any() else float('nan'):.2e}; "
            f"floor median {np.median(floor):.2e} p99 {np.percentile(floor, 99):.2e}; flip rates (gpu, floor) " +
            ", ".join(f">{t:.0e}: {a:.3f} {b:.3f}" for t, (a, b) in rates.items()))
     print(msg)
     assert np.median(e) < median, msg
+    assert calm.sum() >= 0.5 * e.size, msg
+    assert np.percentile(e[calm], 99) < tol, msg
     for t, (a, b) in rates.items():
         assert a <= 2.0 * b + slack, msg
     assert np.percentile(e, 99) <= p99_cap, msg

@@ -83,6 +83,60 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
     assert (0, False, True) in kinds and (2, True, False) in kinds and (2, True, True) in kinds, kinds
 
 
+def test_benched_workload_teacher_forced(dp, ref):
+    """The workload bench.py's headline times: Crossing Field, the
+    reference's default colliders (PianoTask(primitive_fingertip_collisions=False): palm boxes,
+    convex-hull distal colliders; tasks/base.py:101, shadow_hand.py:95,144-152), 4096 envs with
+    staggered episodes (bench.stagger_episodes), uniform random actions. After 12 warm-up steps
+    of the whole launch, 256 sampled envs are stepped teacher-forced against the checker for 5
+    control steps (each from the GPU's state), with the checker's own sensitivity from the
+    limit-preserving 1e-7 rad perturbation (helpers.perturbed): helpers.assert_flip_rates -
+    median < 1e-5, p99 < 1e-4 over the well-conditioned env-steps (floor < 1e-5, at least half),
+    flip rates within 2x the checker's + 1%, p99 < 5e-2; rewards p95 within max(1e-3, 2x the
+    checker's own)."""
+    import sys
+
+    from helpers import ROOT
+    sys.path.insert(0, str(ROOT))
+    from bench import load_song, stagger_episodes
+    N, n, steps = 4096, 256, 5
+    seq, task = load_song(dp, "crossing_field")
+    import dataclasses
+    task = dataclasses.replace(task, primitive_fingertip_collisions=False)
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", seed=12345, canonical_actions=False)
+    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
+    lo, hi = dp.model.action_spec(md)
+    rng, prng = np.random.RandomState(21), np.random.RandomState(22)
+    idx = np.sort(rng.choice(N, n, replace=False))
+    g.reset()
+    stagger_episodes(g, 0, g.song.T)
+    for _ in range(12):
+        g.step(torch.from_numpy(rng.uniform(lo, hi, (N, 45)).astype(np.float32)).cuda())
+    errs, floor, rerr, rfloor, coupled = [], [], [], [], 0
+    for t in range(steps):
+        a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
+        s = {k: v[idx] for k, v in _gs(g).items() if k in KEYS}
+        o.set_state(s)
+        o2.set_state(perturbed(s, prng, md=md))
+        _, rg, _, _ = g.step(torch.from_numpy(a).cuda())
+        coupled += int(g.solver_stats().cpu().numpy()[idx, 4].sum())
+        _, ro, _, _ = o.step(a[idx])
+        _, ro2, _, _ = o2.step(a[idx])
+        qo = o.get_state()["qpos"]
+        errs.append(np.abs(_gs(g)["qpos"][idx] - qo).max(axis=1))
+        floor.append(np.abs(o2.get_state()["qpos"] - qo).max(axis=1))
+        rerr.append(np.abs(rg.cpu().numpy()[idx] - ro))
+        rfloor.append(np.abs(ro2 - ro))
+    e, f = np.concatenate(errs), np.concatenate(floor)
+    assert_flip_rates(e, f, f"bench workload (Crossing Field, box/hull hand, {N} envs), control step; "
+                            f"{coupled} coupled substeps")
+    re, rf = np.concatenate(rerr), np.concatenate(rfloor)
+    print(f"bench workload reward: p95 {np.percentile(re, 95):.3g} floor p95 {np.percentile(rf, 95):.3g}")
+    assert np.percentile(re, 95) <= max(1e-3, 2 * np.percentile(rf, 95))
+    assert coupled > 0  # the sample reached the coupled-hands solve
+
+
 def test_box_hull_hand_one_substep(dp, ref):
     """The reference's default colliders (palm boxes, hull fingertips) at the one-substep gate:
     GPU vs checker for ONE physics substep from the same states (rollout states of the GPU under

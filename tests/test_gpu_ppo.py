@@ -357,6 +357,45 @@ def test_split_rows_kernel_matches_tile_kernel(ppo, tmp_path, monkeypatch, B, tr
         np.testing.assert_allclose(g1[k], g0[k], rtol=0, atol=1e-4 * max(np.abs(g0[k]).max(), 1e-6), err_msg=k)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_split_exchange_timeout_raises_and_applies_nothing(ppo, tmp_path, monkeypatch, graphs):
+    """A timed-out exchange of the column-split rows kernel can no longer reach the weights
+    (ADVICE r5): with the test hook PIANORL_SPLIT_TEST_FAULT=1 member 1 of
+    every group never publishes exchange 0, so the other members' bounded waits (shortened to
+    10 ms by PIANORL_SPLIT_SPIN_TICKS) time out and write the guard word. Then the gradient
+    kernel does not advance the Adam step counts, clip+Adam applies nothing (parameters, moments,
+    step counts bitwise unchanged over the whole update: every minibatch step fails here), and
+    update() raises PianosimError. The guard and the exchange region are re-zeroed, so the next
+    update (hook off) runs and changes the weights."""
+    lib = importlib.import_module("diffusion-piano_amd._lib")
+    rng = np.random.RandomState(5)
+    n, S, B = 512, 329, 128
+    args = (rng.rand(n, S).astype(np.float32), rng.uniform(-1, 1, (n, 45)).astype(np.float32), rng.rand(n),
+            rng.uniform(-60, -40, n).astype(np.float32), rng.rand(n, S).astype(np.float32),
+            (rng.rand(n) < 0.1).astype(np.float32))
+    torch.manual_seed(0)
+    ag = ppo.PPOAgent(S, 45, batch_size=B, ppo_epochs=2, use_wandb=False, checkpoint_dir=str(tmp_path),
+                      graphs=graphs, fused=True)
+    fl = ag.flat
+    before = [t.detach().clone() for t in (fl.param, fl.exp_avg, fl.exp_avg_sq, fl.step_count)]
+    monkeypatch.setenv("PIANORL_SPLIT_SPIN_TICKS", "1000000")
+    monkeypatch.setenv("PIANORL_SPLIT_TEST_FAULT", "1")
+    with pytest.raises(lib.PianosimError, match="timed out"):
+        ag.update(*args)
+    torch.cuda.synchronize()
+    for a, b in zip(before, (fl.param, fl.exp_avg, fl.exp_avg_sq, fl.step_count)):
+        assert torch.equal(a, b)
+    assert int(ag._guard.item()) == 0
+    monkeypatch.delenv("PIANORL_SPLIT_TEST_FAULT")
+    ag._graph = ag._chunk_graph = None  # (a captured graph keeps the hook's launch arguments)
+    ag._graph_eager_left = 2
+    ag.update(*args)
+    torch.cuda.synchronize()
+    assert int(ag._guard.item()) == 0
+    assert not torch.equal(before[0], fl.param)
+    assert torch.isfinite(fl.param).all()
+
+
 def test_rollout_trainer_masks_auto_reset_steps(ppo, tmp_path):
     """An auto-reset step (FIRST: the kernel ignored the action and reset the env) is not a
     transition: the horizon rollout marks it invalid and _prepare drops it after GAE (it enters

@@ -178,6 +178,42 @@ def _bucket_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _guard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = ppo_mod()
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(5, 3), torch.nn.ReLU(), torch.nn.Linear(3, 2))
+        b = m.GradBucket(list(net.parameters()))
+        b.guard = torch.tensor([3 if rank == 1 else 0], dtype=torch.int32)
+        net(torch.full((4, 5), float(rank + 1))).pow(2).sum().backward()
+        b.allreduce_()
+        first = int(b.guard.item())
+        b.guard.zero_()
+        b.allreduce_()  # a clean step after the reset: no rank flagged
+        q.put((rank, first, int(b.guard.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_bucket_carries_the_guard_word_gloo_world2():
+    """The guard word (include/pianorl.h: a failed split-kernel step) rides the gradient
+    all-reduce, so one rank's failure stops every rank's optimiser step: rank 1 flags 3, both
+    ranks come out flagged (rank 1 keeps its code); after clearing, nothing is flagged."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = sorted((q.get(timeout=5) for _ in range(2)), key=lambda t: t[0])
+    assert res == [(0, 1, 0), (1, 3, 0)]
+
+
 def test_grad_bucket_allreduce_gloo_world2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
