@@ -24,7 +24,22 @@ struct XShape {
   float er;
   const uint64_t* cells;  // hull: its support cells (DevModel::x_cell), or nullptr: scan all vertices
   const float4* cellv;    // hull: its support-cell vertex table (DevModel::x_cellv), or nullptr
+  float tie;              // hull: SUP_TIE_HULL x its max vertex norm (x_support's tie band)
 };
+
+// Support ties (oracle/pianosim_ref.c support(), the same rule): MPR's portal directions are
+// often exactly normal to a hull or box face in exact arithmetic, where every vertex of that
+// face is a maximal support and the first-maximal rule picks by the rounding of the dots - a
+// choice that differs between fp32 and fp64 and that no perturbation of the state moves, and
+// which steered 3% of the benched workload's hull contacts to another portal and normal (round
+// 6, tools/contact_diff.py). A hull vertex replaces the running best only when it exceeds it by
+// more than SUP_TIE_HULL x rbound x |d| (~10x the fp32 rounding of a projection; below half the
+// support cells' pruning margin, so the pruned candidate lists still give the full scan's
+// vertex); a box component |dl_i| <= SUP_TIE_BOX max|dl| counts as 0; a capsule axis |ax.d| <=
+// SUP_TIE_CAP |ax||d| as perpendicular.
+constexpr float SUP_TIE_HULL = 2e-6f;
+constexpr float SUP_TIE_BOX = 1e-6f;
+constexpr float SUP_TIE_CAP = 1e-6f;
 
 // a collider moved by -o (its centre, segment and enclosing capsule; rotations, half sizes and
 // hull vertices are frame-relative)
@@ -150,18 +165,23 @@ __device__ __forceinline__ int hull_cell(f3 d) {
 }
 
 // support point in direction d (the CPU checker's support(): box corner by sign, 0 on a zero
-// component; capsule end by sign along the axis + radius along d; hull: first maximal vertex)
+// component; capsule end by sign along the axis + radius along d; hull: first maximal vertex;
+// each with the tie rule above)
+__device__ __forceinline__ float sgn_tie(float x, float band) { return fabsf(x) <= band ? 0.f : sgn0f(x); }
 __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XShape& s, f3 d) {
   if (s.type == 0) {
     const f3 ax = s.p1 - s.p0;
-    const float da = dot3(ax, d), dn = norm3(d);
+    const float dn = norm3(d);
+    float da = dot3(ax, d);
+    if (fabsf(da) <= SUP_TIE_CAP * norm3(ax) * dn) da = 0.f;
     const f3 base = da > 0.f ? s.p1 : (da < 0.f ? s.p0 : (s.p0 + s.p1) * 0.5f);
     return dn > 0.f ? base + d * (s.r / dn) : base;
   }
   const f3 dl = mtv3(s.R, d);
   f3 loc;
   if (s.type == PS_GEOM_BOX) {
-    loc = mk3(sgn0f(dl.x) * s.hs.x, sgn0f(dl.y) * s.hs.y, sgn0f(dl.z) * s.hs.z);
+    const float band = SUP_TIE_BOX * fmaxf(fabsf(dl.x), fmaxf(fabsf(dl.y), fabsf(dl.z)));
+    loc = mk3(sgn_tie(dl.x, band) * s.hs.x, sgn_tie(dl.y, band) * s.hs.y, sgn_tie(dl.z, band) * s.hs.z);
   } else if (s.cellv) {
     // the first maximal vertex over the direction's cell's candidates (x_cellv: the same
     // candidates as x_cell's mask, in the same order, padded by repeats): the cell's 128 bytes
@@ -171,12 +191,13 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
     float4 v[XCV];
 #pragma unroll
     for (int u = 0; u < XCV; u++) v[u] = t[u];
+    const float tie = s.tie * norm3(dl);
     float bd = -INFINITY;
     loc = mk3(0.f, 0.f, 0.f);
 #pragma unroll
     for (int u = 0; u < XCV; u++) {
       const float p = fmaf(dl.z, v[u].z, fmaf(dl.y, v[u].y, dl.x * v[u].x));
-      if (p > bd) { bd = p; loc = mk3(v[u].x, v[u].y, v[u].z); }
+      if (p > bd + tie) { bd = p; loc = mk3(v[u].x, v[u].y, v[u].z); }
     }
   } else if (s.cells) {
     // the first maximal vertex over the candidates of the direction's support cell (x_cell, its
@@ -185,6 +206,7 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
     // direction: every dot is 0, the first vertex.
     const bool zero = dl.x == 0.f && dl.y == 0.f && dl.z == 0.f;
     uint64_t msk = zero ? 1ull : s.cells[hull_cell(dl)];
+    const float tie = s.tie * norm3(dl);
     float bd = -INFINITY;
     loc = mk3(0.f, 0.f, 0.f);
     while (msk) {
@@ -201,32 +223,24 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         const float p = fmaf(dl.z, v[u].z, fmaf(dl.y, v[u].y, dl.x * v[u].x));
-        if (ok[u] && p > bd) { bd = p; loc = v[u]; }
+        if (ok[u] && p > bd + tie) { bd = p; loc = v[u]; }
       }
     }
   } else {
-    // the first maximal vertex, eight at a time: the block's loads issued together, its best by
-    // a 3-level tree (ties to the lower index), then against the running best (ties to the
-    // earlier block) - the sequential scan's choice with an 11-deep compare chain per block
-    // instead of 8 and the loads off the chain
+    // every vertex in order (the harness's reference scan; the step kernel has the cells),
+    // eight loads issued together
+    const float tie = s.tie * norm3(dl);
     float bd = -INFINITY;
     loc = mk3(0.f, 0.f, 0.f);
     for (int i0 = 0; i0 < s.nv; i0 += 8) {
       float4 v[8];
-      float p[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + min(i0 + j, s.nv - 1)]);
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        v[j] = *reinterpret_cast<const float4*>(m->hull_v[s.v0 + min(i0 + j, s.nv - 1)]);
-        p[j] = i0 + j < s.nv ? fmaf(dl.z, v[j].z, fmaf(dl.y, v[j].y, dl.x * v[j].x)) : -INFINITY;
+        const float p = fmaf(dl.z, v[j].z, fmaf(dl.y, v[j].y, dl.x * v[j].x));
+        if (i0 + j < s.nv && p > bd + tie) { bd = p; loc = mk3(v[j].x, v[j].y, v[j].z); }
       }
-#pragma unroll
-      for (int w = 1; w < 8; w *= 2) {
-#pragma unroll
-        for (int j = 0; j < 8; j += 2 * w) {
-          if (p[j + w] > p[j]) { p[j] = p[j + w]; v[j] = v[j + w]; }
-        }
-      }
-      if (p[0] > bd) { bd = p[0]; loc = mk3(v[0].x, v[0].y, v[0].z); }
     }
   }
   return s.c + mv3(s.R, loc);
@@ -284,25 +298,38 @@ __device__ __forceinline__ void expand_portal(const MprPt& p0, MprPt& p1, MprPt&
     if (dot3(p3.v, v4v0) > 0.f) p2 = v4; else p1 = v4;
   }
 }
-// closest point of triangle (a, b, c) to the origin (Ericson, RTCD 5.1.5)
-__device__ __forceinline__ f3 tri_closest_origin(f3 a, f3 b, f3 c) {
-  const f3 ab = b - a, ac = c - a, ap = a * -1.f;
-  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-  if (d1 <= 0.f && d2 <= 0.f) return a;
-  const f3 bp = b * -1.f;
-  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-  if (d3 >= 0.f && d4 <= d3) return b;
-  const float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + ab * (d1 / (d1 - d3));
-  const f3 cp = c * -1.f;
-  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
-  if (d6 >= 0.f && d5 <= d6) return c;
-  const float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + ac * (d2 / (d2 - d6));
-  const float va = d3 * d6 - d5 * d4;
-  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + (c - b) * ((d4 - d3) / ((d4 - d3) + (d5 - d6)));
-  const float den = 1.f / (va + vb + vc);
-  return a + ab * (vb * den) + ac * (vc * den);
+// closest point of triangle (a, b, c) to the origin (Ericson, RTCD 5.1.5), in fp64: MPR's final
+// portal is a small triangle (sub-mm edges) ~1 mm from the origin, and the fp32 form's
+// cancellations in the region tests and barycentric weights put the closest point on a wrong
+// vertex or edge - its direction, the contact normal, off by up to ~0.4 rad (round 6,
+// tools/contact_diff.py); the closest point itself is 1-Lipschitz in the vertices, so from the
+// fp32 portal points the fp64 form is accurate to their rounding. Once per MPR call.
+__device__ __forceinline__ f3 tri_closest_origin_d(f3 af, f3 bf, f3 cf) {
+  const double ax = af.x, ay = af.y, az = af.z, bx = bf.x, by = bf.y, bz = bf.z, cx = cf.x, cy = cf.y, cz = cf.z;
+  const double abx = bx - ax, aby = by - ay, abz = bz - az, acx = cx - ax, acy = cy - ay, acz = cz - az;
+  const double d1 = -(abx * ax + aby * ay + abz * az), d2 = -(acx * ax + acy * ay + acz * az);
+  if (d1 <= 0.0 && d2 <= 0.0) return af;
+  const double d3 = -(abx * bx + aby * by + abz * bz), d4 = -(acx * bx + acy * by + acz * bz);
+  if (d3 >= 0.0 && d4 <= d3) return bf;
+  const double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {
+    const double t = d1 / (d1 - d3);
+    return mk3((float)(ax + abx * t), (float)(ay + aby * t), (float)(az + abz * t));
+  }
+  const double d5 = -(abx * cx + aby * cy + abz * cz), d6 = -(acx * cx + acy * cy + acz * cz);
+  if (d6 >= 0.0 && d5 <= d6) return cf;
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+    const double t = d2 / (d2 - d6);
+    return mk3((float)(ax + acx * t), (float)(ay + acy * t), (float)(az + acz * t));
+  }
+  const double va = d3 * d6 - d5 * d4;
+  if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0) {
+    const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    return mk3((float)(bx + (cx - bx) * t), (float)(by + (cy - by) * t), (float)(bz + (cz - bz) * t));
+  }
+  const double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
+  return mk3((float)(ax + abx * v + acx * w), (float)(ay + aby * v + acy * w), (float)(az + abz * v + acz * w));
 }
 __device__ __forceinline__ f3 mpr_pos(const MprPt& p0, const MprPt& p1, const MprPt& p2, const MprPt& p3) {
   const f3 dir = portal_dir(p1, p2, p3);
@@ -380,7 +407,7 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
     dir = portal_dir(p1, p2, p3);
     const MprPt v4 = mpr_sup_t<PAIR>(m, A, B, own, role, dir);
     if (portal_reach_tol(p1, p2, p3, v4, dir) || it > MPR_MAXITF) {
-      const f3 cp = tri_closest_origin(p1.v, p2.v, p3.v);
+      const f3 cp = tri_closest_origin_d(p1.v, p2.v, p3.v);
       *depth = norm3(cp);
       *n = mpr_zero(*depth) ? dir : cp * (1.f / *depth);
       *pos = mpr_pos(p0, p1, p2, p3);

@@ -103,9 +103,12 @@ class TaskConfig:
     constraint_solver: str = "newton"
     solver_iterations: Optional[int] = None
     # 0: the solve ends when its line search ends in the Hessian's piece (the exact minimiser, to
-    # the fp32 factor's error); 1: one more Newton step in that piece on coupled-hand substeps;
-    # 2: on every substep (tighter fp32 parity for ~5-8% of the throughput; ps_task_cfg.solver_refine)
-    solver_refine: int = 0
+    # the fp32 factor's error); 1 (the default since round 6): one more Newton step in that piece
+    # on coupled-hand substeps - the fp32 parity target of 1e-4 over all env-steps of the coupled /
+    # heavy-contact / Guren cases needs it, ~5% of the throughput; 2: on
+    # every substep. Solves that end in the previous substep's guessed piece are not refined
+    # (ps_task_cfg.solver_refine)
+    solver_refine: int = 1
     max_contacts: int = 20
     hand_xml: Optional[str] = None  # a user hand MJCF (path or text, mjcf.load_hand); None = authored hand
     # PianoTask keyword arguments (tasks/base.py:96-107, forwarded by PianoWithShadowHands'

@@ -214,12 +214,14 @@ typedef struct {
   int32_t solver;                   /* PS_SOLVER_NEWTON (the only value) */
   int32_t randomize_hand_positions; /* piano_with_shadow_hands.py:64,491-499: each episode shifts
                                        both hands by the same U(-0.05, 0.05) m along y */
-  int32_t solver_refine;            /* 0 (default): the Newton solve ends when its line search ends in
-                                       the Hessian's piece; 1: then one more (refining) Newton step
-                                       in that piece on the substeps whose hands are coupled, 2: on
-                                       every substep - the fp32 solve's error shrinks (teacher-forced
-                                       qpos p99 against the fp64 checker ~1.5e-4 -> ~8e-5 on coupled
-                                       states) at ~5-8% of the throughput */
+  int32_t solver_refine;            /* 0: the Newton solve ends when its line search ends in the
+                                       Hessian's piece; 1 (TaskConfig's default since round 6): then
+                                       one more (refining) Newton step in that piece on the substeps
+                                       whose hands are coupled, 2: on every substep - the fp32 solve's
+                                       error shrinks (teacher-forced qpos p99 against the fp64 checker
+                                       ~1.5e-4 -> ~8e-5 on coupled states) at ~5% of the throughput
+                                       (DESIGN.md section 5). A solve that ends in the previous
+                                       substep's guessed piece (one checked step) is not refined. */
 } ps_task_cfg;
 #define PS_TASK_CFG_SIZE ((uint32_t)sizeof(ps_task_cfg))
 

@@ -642,31 +642,54 @@ typedef struct {
   double hs[3];
   const double (*vert)[3];
   int nvert;
+  double rb;           /* hull: max vertex norm (xgeom_rbound), the scale of its support ties */
 } shape;
 
 static double sgn0(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
 
+/* Support ties. MPR's portal directions are often EXACTLY normal to a face of a collider in
+ * exact arithmetic - a portal triangle of three vertices of one hull face (or box face) minus
+ * one point of the other shape has that face's normal - and then every vertex of the face
+ * is a maximal support. libccd's first-maximal rule then picks whichever vertex the rounding
+ * of the dots favours: a choice no perturbation of the state moves (the tie moves with the
+ * body), that differs between fp64 and fp32 arithmetic, and that changes the portal path and
+ * the final normal (by up to ~0.5 here: round 6, tools/contact_diff.py, 3% of the hull
+ * contacts of the benched workload). Ties are therefore broken by a tolerance, identically in
+ * the kernel (csrc/collide_x.h x_support): a hull vertex replaces the running best only when
+ * its projection exceeds it by more than SUP_TIE_HULL x rb x |d| (the earliest vertex wins
+ * inside the band; 2e-6 rb: ~10x the fp32 rounding of a projection, below half the support
+ * cells' pruning margin of 1e-5 rb, so the pruned candidate lists give the same vertex); a box
+ * component |dl_i| <= SUP_TIE_BOX max|dl| counts as 0 (the face centre: a support within 1e-6
+ * of the box size); a capsule axis |ax.d| <= SUP_TIE_CAP |ax||d| as perpendicular (the
+ * midpoint). Every choice is a support to within 2e-8 m, far inside MPR's 1e-6 m tolerance. */
+#define SUP_TIE_HULL 2e-6
+#define SUP_TIE_BOX 1e-6
+#define SUP_TIE_CAP 1e-6
+
 /* support point of the shape in direction d (MuJoCo's mjccd_support: box corner by the sign
  * of each local component, 0 on a zero component; capsule end by the sign along the axis
- * plus the radius along d; hull: first vertex of maximal projection) */
+ * plus the radius along d; hull: first vertex of maximal projection - each with the tie
+ * tolerance above) */
 static v3 support(const shape* s, v3 d) {
   if (s->type == 0) {
     v3 ax = sub(s->p1, s->p0);
-    double dn = nrm(d);
-    v3 base = dot(ax, d) >= 0.0 ? s->p1 : s->p0;
-    if (dot(ax, d) == 0.0) base = scl(add(s->p0, s->p1), 0.5);
+    double dn = nrm(d), da = dot(ax, d);
+    if (fabs(da) <= SUP_TIE_CAP * nrm(ax) * dn) da = 0.0;
+    v3 base = da > 0.0 ? s->p1 : (da < 0.0 ? s->p0 : scl(add(s->p0, s->p1), 0.5));
     return dn > 0.0 ? add(base, scl(d, s->r / dn)) : base;
   }
   v3 dl = mtv(s->R, d);
   v3 loc;
   if (s->type == PS_GEOM_BOX) {
-    loc = mk(sgn0(dl.v[0]) * s->hs[0], sgn0(dl.v[1]) * s->hs[1], sgn0(dl.v[2]) * s->hs[2]);
+    double mx = fmax(fabs(dl.v[0]), fmax(fabs(dl.v[1]), fabs(dl.v[2]))), sg[3];
+    for (int k = 0; k < 3; k++) sg[k] = fabs(dl.v[k]) <= SUP_TIE_BOX * mx ? 0.0 : sgn0(dl.v[k]);
+    loc = mk(sg[0] * s->hs[0], sg[1] * s->hs[1], sg[2] * s->hs[2]);
   } else {
     int best = 0;
-    double bd = -INFINITY;
+    double bd = -INFINITY, tie = SUP_TIE_HULL * s->rb * nrm(dl);
     for (int i = 0; i < s->nvert; i++) {
       double p = dl.v[0] * s->vert[i][0] + dl.v[1] * s->vert[i][1] + dl.v[2] * s->vert[i][2];
-      if (p > bd) { bd = p; best = i; }
+      if (p > bd + tie) { bd = p; best = i; }
     }
     loc = mk(s->vert[best][0], s->vert[best][1], s->vert[best][2]);
   }
@@ -953,6 +976,7 @@ static shape extra_shape(const envdata* E, int h, int i, const ps_model_desc* d)
   for (int k = 0; k < 3; k++) s.hs[k] = d->xgeom_size[h][i][k];
   s.vert = (const double(*)[3])d->hull_vert[h][d->xgeom_vert[h][i][0]];
   s.nvert = d->xgeom_vert[h][i][1];
+  s.rb = d->xgeom_rbound[h][i];
   return s;
 }
 static shape box_shape(v3 c, m3 R, const double* hs) {
@@ -2149,6 +2173,8 @@ static shape unpack_shape(const double* p, const double* verts, int nv) {
   for (int i = 0; i < 3; i++) s.hs[i] = p[20 + i];
   s.vert = (const double(*)[3])verts;
   s.nvert = nv;
+  s.rb = 0.0;
+  for (int i = 0; i < nv; i++) s.rb = fmax(s.rb, nrm(mk(verts[3 * i], verts[3 * i + 1], verts[3 * i + 2])));
   if (s.type == 0) s.c = scl(add(s.p0, s.p1), 0.5);
   return s;
 }

@@ -146,6 +146,7 @@ class OracleEnv:
         ``seed``: key of the randomize_hand_positions draws (as ps_create's); ``env_offset``: the
         global id of env 0 (as ps_set_env_offset)."""
         self._L = flops_lib() if counting else lib()
+        self._counting = counting
         from importlib import import_module
         abi = import_module("diffusion-piano_amd.abi")
         self._song = song_tables
@@ -177,9 +178,13 @@ class OracleEnv:
         self._L.ref_reset(self._h, m, obs)
         return obs
 
-    def step(self, action, threads: int = 1):
+    def step(self, action, threads: int = None):
         """One control step of every env; ``threads > 1`` spreads the envs over OpenMP
-        threads (the all-cores CPU baseline; results identical to the serial loop)."""
+        threads (the all-cores CPU baseline; results identical to the serial loop). Default:
+        ORACLE_THREADS, else up to 8 of this process's CPUs for 16+ envs (serial when counting
+        FLOPs or solver statistics, whose counters are process-wide)."""
+        if threads is None:
+            threads = 1 if (self.n < 16 or self._counting) else _default_threads()
         a = np.ascontiguousarray(action, np.float32).reshape(self.n, self.action_dim)
         obs = np.zeros((self.n, self.obs_dim), np.float32)
         rew = np.zeros(self.n, np.float32)
@@ -280,6 +285,14 @@ class OracleEnv:
 
     def physics_substep(self):
         self._L.ref_physics_substep(self._h)
+
+
+def _default_threads() -> int:
+    import os
+    v = os.environ.get("ORACLE_THREADS")
+    if v:
+        return max(1, int(v))
+    return max(1, min(8, len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "8"))))
 
 
 def hand_offset_draw(seed: int, env: int, episode: int) -> float:

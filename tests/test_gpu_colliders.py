@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import assert_flip_rates, box_hull_hand, perturbed, song
+from helpers import Floor, assert_flip_rates, box_hull_hand, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -47,8 +47,7 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
     seq = song(dp, "twinkle")
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
-    o = ref.OracleEnv(md, st, tc, n)
-    o2 = ref.OracleEnv(md, st, tc, n)
+    o, o2 = ref.OracleEnv(md, st, tc, n), Floor(ref, md, st, tc, n)
     lo, hi = dp.model.action_spec(md)
     rng = np.random.RandomState(5)
     prng = np.random.RandomState(9)
@@ -58,13 +57,13 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
         a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
         s = {k: v for k, v in _gs(g).items() if k in KEYS}
         o.set_state(s)
-        o2.set_state(perturbed(s, prng))
+        o2.set_state(s, prng)
         _, rg, _, _ = g.step(torch.from_numpy(a).cuda())
         _, ro, _, _ = o.step(a)
         _, ro2, _, _ = o2.step(a)
         qo = o.get_state()["qpos"]
         errs.append(np.abs(_gs(g)["qpos"] - qo).max(axis=1))
-        floor.append(np.abs(o2.get_state()["qpos"] - qo).max(axis=1))
+        floor.append(o2.dev(qo))
         rerr.append(np.abs(rg.cpu().numpy() - ro))
         rfloor.append(np.abs(ro2 - ro))
         ncg.append(g.contact_count().cpu().numpy())
@@ -105,7 +104,7 @@ def test_benched_workload_teacher_forced(dp, ref):
     task = dataclasses.replace(task, primitive_fingertip_collisions=False)
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", seed=12345, canonical_actions=False)
-    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
+    o, o2 = ref.OracleEnv(md, st, tc, n), Floor(ref, md, st, tc, n)
     lo, hi = dp.model.action_spec(md)
     rng, prng = np.random.RandomState(21), np.random.RandomState(22)
     idx = np.sort(rng.choice(N, n, replace=False))
@@ -118,14 +117,14 @@ def test_benched_workload_teacher_forced(dp, ref):
         a = rng.uniform(lo, hi, (N, 45)).astype(np.float32)
         s = {k: v[idx] for k, v in _gs(g).items() if k in KEYS}
         o.set_state(s)
-        o2.set_state(perturbed(s, prng, md=md))
+        o2.set_state(s, prng)
         _, rg, _, _ = g.step(torch.from_numpy(a).cuda())
         coupled += int(g.solver_stats().cpu().numpy()[idx, 4].sum())
         _, ro, _, _ = o.step(a[idx])
         _, ro2, _, _ = o2.step(a[idx])
         qo = o.get_state()["qpos"]
         errs.append(np.abs(_gs(g)["qpos"][idx] - qo).max(axis=1))
-        floor.append(np.abs(o2.get_state()["qpos"] - qo).max(axis=1))
+        floor.append(o2.dev(qo))
         rerr.append(np.abs(rg.cpu().numpy()[idx] - ro))
         rfloor.append(np.abs(ro2 - ro))
     e, f = np.concatenate(errs), np.concatenate(floor)
@@ -152,7 +151,7 @@ def test_box_hull_hand_one_substep(dp, ref):
     assert md.n_substeps == 1
     roll = dp.BatchedPianoEnv(n, seq, task10, device="cuda:0", canonical_actions=False)
     g = dp.BatchedPianoEnv(n, seq, task1, device="cuda:0", canonical_actions=False)
-    o, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
+    o, o2 = ref.OracleEnv(md, st, tc, n), Floor(ref, md, st, tc, n)
     lo, hi = dp.model.action_spec(md)
     rng, prng = np.random.RandomState(6), np.random.RandomState(7)
     roll.reset()
@@ -163,13 +162,13 @@ def test_box_hull_hand_one_substep(dp, ref):
         a = rng.uniform(lo, hi, (n, 45)).astype(np.float32)
         g.set_state(s)
         o.set_state(s)
-        o2.set_state(perturbed(s, prng))
+        o2.set_state(s, prng)
         g.step(torch.from_numpy(a).cuda())
         o.step(a)
         o2.step(a)
         sg, so = _gs(g), o.get_state()
         eq.append(np.abs(sg["qpos"] - so["qpos"]).max(axis=1))
-        fq.append(np.abs(o2.get_state()["qpos"] - so["qpos"]).max(axis=1))
+        fq.append(o2.dev(so["qpos"]))
         v0 = s["qvel"].astype(np.float64)
         acc_o, acc_g = (so["qvel"] - v0) / 0.005, (sg["qvel"] - v0) / 0.005
         ea.append(np.abs(acc_g - acc_o).max(axis=1) / np.maximum(np.abs(acc_o).max(axis=1), 1.0))

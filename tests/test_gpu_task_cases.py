@@ -15,7 +15,7 @@
 import numpy as np
 import pytest
 
-from helpers import assert_parity, perturbed, song
+from helpers import Floor, assert_parity, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -93,21 +93,21 @@ def test_guren_at_4096_envs(dp, ref):
     assert torch.equal(s["qpos"][: N // 2], s["qpos"][N // 2:]) and torch.equal(obs[: N // 2], obs[N // 2:])
     # 256 sampled envs, teacher-forced for 4 steps against the oracle (1024 env-steps)
     idx = np.arange(0, N, N // 256)
-    o, o2 = ref.OracleEnv(md, st, tc, len(idx)), ref.OracleEnv(md, st, tc, len(idx))
+    o, o2 = ref.OracleEnv(md, st, tc, len(idx)), Floor(ref, md, st, tc, len(idx))
     prng = np.random.RandomState(6)
     lay = dp.obs_layout(tc)
     eqs, ers, fl = [], [], []
     for _ in range(4):
         sg = _gs(g)
         o.set_state({k: sg[k][idx] for k in KEYS})
-        o2.set_state(perturbed({k: sg[k][idx] for k in KEYS}, prng))
+        o2.set_state({k: sg[k][idx] for k in KEYS}, prng)
         a = lo + torch.rand(N, 45, device="cuda:0", generator=gen) * (hi - lo)
         og, rg, _, tg = g.step(a)
         oo, ro, _, to = o.step(a.cpu().numpy()[idx])
         o2.step(a.cpu().numpy()[idx])
         np.testing.assert_array_equal(tg.cpu().numpy()[idx], to)
         eqs.append(np.abs(g.get_state()["qpos"].cpu().numpy()[idx] - o.get_state()["qpos"]).max(axis=1))
-        fl.append(np.abs(o2.get_state()["qpos"] - o.get_state()["qpos"]).max(axis=1))
+        fl.append(o2.dev(o.get_state()["qpos"]))
         ers.append(np.abs(rg.cpu().numpy()[idx] - ro))
         np.testing.assert_array_equal(og.cpu().numpy()[idx][:, lay["fingering"]], oo[:, lay["fingering"]])
     eq, er = np.concatenate(eqs), np.concatenate(ers)

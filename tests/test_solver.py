@@ -55,7 +55,7 @@ def test_pgs_solver_is_retired(dp):
     with pytest.raises(ValueError, match="retired"):
         dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(constraint_solver="pgs"))
     _, _, tc = dp.compile_task(song(dp, "twinkle"), dp.TaskConfig(constraint_solver="exact"))
-    assert tc.solver == 1 and tc.solver_iterations == 0 and tc.solver_refine == 0
+    assert tc.solver == 1 and tc.solver_iterations == 0 and tc.solver_refine == 1
 
 
 def test_solver_refine_option(dp):

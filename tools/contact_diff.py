@@ -38,17 +38,29 @@ def kind_of(c, ncap=40):
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-    seq, task = load_song(dp, "crossing_field")
-    task = dataclasses.replace(task, primitive_fingertip_collisions=False)
+    mode = sys.argv[3] if len(sys.argv) > 3 else "bench"
+    if mode == "bench":
+        seq, task = load_song(dp, "crossing_field")
+        task = dataclasses.replace(task, primitive_fingertip_collisions=False)
+    else:  # "random": random joint states of the all-capsule hand (tests/helpers.random_states)
+        from helpers import random_states, song
+        seq, task = song(dp, "twinkle"), dp.TaskConfig(control_timestep=0.005)
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
     g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", seed=12345, canonical_actions=False)
     g.record_contacts(True)
     lo, hi = dp.model.action_spec(md)
     rng = np.random.RandomState(3)
     g.reset()
-    stagger_episodes(g, 0, g.song.T)
-    for _ in range(steps):
-        g.step(torch.from_numpy(rng.uniform(lo, hi, (N, 45)).astype(np.float32)).cuda())
+    if mode == "bench":
+        stagger_episodes(g, 0, g.song.T)
+        for _ in range(steps):
+            g.step(torch.from_numpy(rng.uniform(lo, hi, (N, 45)).astype(np.float32)).cuda())
+    else:
+        q, v = random_states(md, N, rng, vscale=0.1)
+        q[:, :88] = np.clip(q[:, :88], 0.0, None)
+        g.set_state(dict(qpos=q, qvel=v, qacc_ws=np.zeros_like(q), ctrl=np.zeros((N, 44)), sustain=np.zeros(N),
+                         t_idx=np.zeros(N, np.int32), last=np.zeros(N, np.uint8)))
+        g.step(torch.zeros(N, 45, device="cuda:0"))
     s = {k: v.cpu().numpy() for k, v in g.get_state().items() if k in KEYS}
     cg = g.contacts()
     o = ref.OracleEnv(md, st, tc, N)

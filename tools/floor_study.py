@@ -36,7 +36,7 @@ from helpers import DATA, perturb_joints, song  # noqa: E402
 from bench import load_song, stagger_episodes  # noqa: E402
 
 KEYS = ("qpos", "qvel", "qacc_ws", "ctrl", "sustain", "t_idx", "last")
-REFINE = int(os.environ.get("PIANOSIM_REFINE", "0"))
+REFINE = int(os.environ.get("PIANOSIM_REFINE", "1"))
 K = 3
 THREADS = int(os.environ.get("FLOOR_THREADS", "16"))
 

@@ -30,7 +30,7 @@ from helpers import DATA, perturbed, song  # noqa: E402
 import test_gpu_solver as ts  # noqa: E402
 
 KEYS = ts.KEYS
-REFINE = int(os.environ.get("PIANOSIM_REFINE", "0"))  # the GPU env's TaskConfig.solver_refine
+REFINE = int(os.environ.get("PIANOSIM_REFINE", "1"))  # the GPU env's TaskConfig.solver_refine
 
 
 def _stats(e, floor=None):

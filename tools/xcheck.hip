@@ -14,7 +14,7 @@ using namespace ps;
 // packed collider (as ref_narrow): type, centre 3, row-major R 9, p0 3, p1 3, r, half sizes 3,
 // hull first vertex, vertex count (25 floats)
 constexpr int PK = 25;
-__device__ XShape unpack(const float* p, const uint64_t* cells, const float4* table, const int* tok) {
+__device__ XShape unpack(const DevModel* m, const float* p, const uint64_t* cells, const float4* table, const int* tok) {
   XShape s;
   s.type = (int)p[0];
   s.c = ld3(p + 1);
@@ -30,6 +30,9 @@ __device__ XShape unpack(const float* p, const uint64_t* cells, const float4* ta
   s.cellv = table && s.type == PS_GEOM_HULL && tok[s.v0] ? table + (size_t)s.v0 * (XNCELL + 1) * XCV : nullptr;
   if (s.type == 0) s.c = (s.p0 + s.p1) * 0.5f;
   s.e0 = s.e1 = s.c;
+  float rb = 0.f;  // the hull's max vertex norm (DevModel::x_rb in the step kernel)
+  for (int i = 0; s.type == PS_GEOM_HULL && i < s.nv; i++) rb = fmaxf(rb, norm3(ld3(m->hull_v[s.v0 + i])));
+  s.tie = SUP_TIE_HULL * rb;
   return s;
 }
 
@@ -41,7 +44,7 @@ __global__ void xcheck_kernel(const DevModel* m, const uint64_t* cells, const fl
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = PAIR ? t >> 1 : t;
   if (i >= n) return;
-  const XShape A = unpack(a + PK * i, cells, table, tok), B = unpack(b + PK * i, cells, table, tok);
+  const XShape A = unpack(m, a + PK * i, cells, table, tok), B = unpack(m, b + PK * i, cells, table, tok);
   f3 pos[BB_MAXPT], nrm[BB_MAXPT];
   float dist[BB_MAXPT];
   bool swap;
