@@ -86,7 +86,7 @@ def _run(dp, ref, kind, workload):
     # teacher-forced: re-sync every step; o2 from the perturbed state (the checker's sensitivity)
     g.reset()
     o.reset()
-    o2 = Floor(ref, *dp.compile_task(*_task(dp, workload), canonical_actions=False), N)
+    o2 = Floor(ref, *dp.compile_task(*_task(dp, workload), canonical_actions=False), N, k=3)  # (8 envs: cheap)
     prng = np.random.RandomState(4)
     floor = []
     for t in range(200):
