@@ -26,7 +26,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 sys.path.insert(0, str(ROOT / "oracle"))
 dp = importlib.import_module("diffusion-piano_amd")
 import ref  # noqa: E402  (oracle/ref.py, test infrastructure)
-from helpers import DATA, perturbed, song  # noqa: E402
+from helpers import DATA, Floor, perturbed, song  # noqa: E402
 import test_gpu_solver as ts  # noqa: E402
 
 KEYS = ts.KEYS
@@ -48,8 +48,8 @@ def _stats(e, floor=None):
 
 def case_bench():
     md, g, o = ts._pair(dp, ref, "crossing_field", 64, solver_refine=REFINE)
-    o2 = ref.OracleEnv(*dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True),
-                                        canonical_actions=False), 64)
+    o2 = Floor(ref, *dp.compile_task(song(dp, "crossing_field"), dp.TaskConfig(trim_silence=True),
+                                     canonical_actions=False), 64)
     return _stats(*ts._teacher_forced(md, g, o, o2, 16, np.random.RandomState(21)))
 
 
