@@ -247,3 +247,29 @@ def test_oracle_rollout_with_box_and_hull_colliders(dp, ref):
     s = o.get_state()
     assert np.isfinite(s["qpos"]).all() and np.isfinite(s["qvel"]).all()
     assert {("key", "x"), ("x", "c"), ("x", "x")} <= kinds, kinds
+
+
+def test_mpr_support_ties_are_stable(ref, dp):
+    """Support ties (round 6): a fingertip hull resting on a key box with
+    a face exactly parallel to the key's top (and a cube hull face-down on a box) puts MPR's
+    portal directions exactly normal to tied faces. The tie-tolerant support must make the
+    result a continuous function of the input there: 1e-12 m moves of the hull give the same
+    contact to 1e-9 (first-maximal picks by rounding noise and could switch the portal). The
+    GPU side of the same rule: tests/test_gpu_colliders.py::test_benched_workload_contact_lists."""
+    rng = np.random.RandomState(0)
+    _, tip = dp.mjcf.convex_hull_collider(capsule_points(0.0085, 0.006))
+    for verts, hs, lift in ((CUBE * 0.01, (0.0117, 0.0235, 0.0113), 0.01), (tip, (0.0117, 0.0235, 0.0113), None)):
+        for trial in range(20):
+            yaw = rng.uniform(0, 2 * math.pi) if trial % 2 else 0.0
+            R = rot((0, 0, 1), yaw)
+            if lift is None:  # the tip hull's lowest point just below the key's top
+                lift = -np.min(verts[:, 2])
+            c = np.array([rng.uniform(-0.005, 0.005), rng.uniform(-0.01, 0.01), 0.0113 + lift - 5e-4])
+            A = ref.shape("box", c=(0, 0, 0), hs=hs)
+            base = ref.narrow(A, ref.shape("hull", c=c, R=R, verts=verts))
+            assert len(base) == 1
+            for _ in range(8):
+                moved = ref.narrow(A, ref.shape("hull", c=c + rng.normal(0, 1e-12, 3), R=R, verts=verts))
+                assert len(moved) == 1
+                (p0, n0, d0), (p1, n1, d1) = base[0], moved[0]
+                assert np.abs(n1 - n0).max() < 1e-9 and abs(d1 - d0) < 1e-9 and np.abs(p1 - p0).max() < 1e-9

@@ -318,3 +318,62 @@ def test_narrow_phase_matches_checker(dp, ref):
     # on ties: both rare
     assert len(bad) <= 0.01 * counted, bad[:10]
     assert hits > 500
+
+
+def test_benched_workload_contact_lists(dp, ref):
+    """The narrow phases on the bench's workload, contact by contact (round 6): 4096 staggered
+    Crossing Field envs with the reference's default colliders after 8 random-action steps; the
+    GPU's contact list of each env (its task-layer collision pass at the end state,
+    ps_record_contacts) against the checker's collision pass at the same fp32 state. A contact
+    present on one side only, or with distance off by > 1e-5 m, normal by > 1e-3 or point by >
+    1e-4 m, is a mismatch. Before round 6's support-tie tolerance and fp64 closest point 202 of
+    ~13.6K contacts mismatched (all with a hull, normals off by up to 0.5); measured after: 12-17
+    (MPR's termination test on capsule-hull pairs, parallel forearm capsules). Gate: at most 0.3%
+    of the contacts, and none from a pair kind that never mismatches (box-box, hull-key)."""
+    import sys
+    from collections import Counter
+
+    from helpers import ROOT
+    sys.path.insert(0, str(ROOT))
+    from bench import load_song, stagger_episodes
+    N = 4096
+    seq, task = load_song(dp, "crossing_field")
+    import dataclasses
+    task = dataclasses.replace(task, primitive_fingertip_collisions=False)
+    md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
+    g = dp.BatchedPianoEnv(N, seq, task, device="cuda:0", seed=12345, canonical_actions=False)
+    g.record_contacts(True)
+    lo, hi = dp.model.action_spec(md)
+    rng = np.random.RandomState(3)
+    g.reset()
+    stagger_episodes(g, 0, g.song.T)
+    for _ in range(8):
+        g.step(torch.from_numpy(rng.uniform(lo, hi, (N, 45)).astype(np.float32)).cuda())
+    s = {k: v for k, v in _gs(g).items() if k in KEYS}
+    cg = g.contacts()
+    o = ref.OracleEnv(md, st, tc, N)
+    o.set_state(s)
+    total, bad = 0, Counter()
+    for i in range(N):
+        co = o.contacts_full(i)
+        used = set()
+        for c in co:
+            total += 1
+            kind = "key" if c[0] == 0 else ("base" if c[0] == 1 else "hand-hand")
+            match = [j for j, x in enumerate(cg[i]) if x[:4] == c[:4] and j not in used]
+            if not match:
+                bad[("checker only", kind)] += 1
+                continue
+            j = min(match, key=lambda j: np.abs(cg[i][j][5] - c[5]).max())
+            used.add(j)
+            x = cg[i][j]
+            if abs(x[4] - c[4]) > 1e-5 or np.abs(x[5] - c[5]).max() > 1e-4 or np.abs(x[6] - c[6]).max() > 1e-3:
+                bad[("differs", kind)] += 1
+        for j, x in enumerate(cg[i]):
+            if j not in used and not [c for c in co if c[:4] == x[:4]]:
+                bad[("GPU only", "key" if x[0] == 0 else ("base" if x[0] == 1 else "hand-hand"))] += 1
+    nbad = sum(bad.values())
+    print(f"bench workload contact lists: {total} contacts, {nbad} mismatches {dict(bad)}")
+    assert total > 10000
+    assert nbad <= 0.003 * total, dict(bad)
+    assert all(kind == "hand-hand" for _, kind in bad), dict(bad)
