@@ -168,15 +168,8 @@ __device__ __forceinline__ int hull_cell(f3 d) {
 // component; capsule end by sign along the axis + radius along d; hull: first maximal vertex;
 // each with the tie rule above)
 __device__ __forceinline__ float sgn_tie(float x, float band) { return fabsf(x) <= band ? 0.f : sgn0f(x); }
-__device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XShape& s, f3 d) {
-  if (s.type == 0) {
-    const f3 ax = s.p1 - s.p0;
-    const float dn = norm3(d);
-    float da = dot3(ax, d);
-    if (fabsf(da) <= SUP_TIE_CAP * norm3(ax) * dn) da = 0.f;
-    const f3 base = da > 0.f ? s.p1 : (da < 0.f ? s.p0 : (s.p0 + s.p1) * 0.5f);
-    return dn > 0.f ? base + d * (s.r / dn) : base;
-  }
+// box / hull: the support in the collider's own frame (box corner, hull vertex)
+__device__ __forceinline__ f3 x_support_local(const DevModel* __restrict__ m, const XShape& s, f3 d) {
   const f3 dl = mtv3(s.R, d);
   f3 loc;
   if (s.type == PS_GEOM_BOX) {
@@ -243,7 +236,18 @@ __device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XS
       }
     }
   }
-  return s.c + mv3(s.R, loc);
+  return loc;
+}
+__device__ __forceinline__ f3 x_support(const DevModel* __restrict__ m, const XShape& s, f3 d) {
+  if (s.type == 0) {
+    const f3 ax = s.p1 - s.p0;
+    const float dn = norm3(d);
+    float da = dot3(ax, d);
+    if (fabsf(da) <= SUP_TIE_CAP * norm3(ax) * dn) da = 0.f;
+    const f3 base = da > 0.f ? s.p1 : (da < 0.f ? s.p0 : (s.p0 + s.p1) * 0.5f);
+    return dn > 0.f ? base + d * (s.r / dn) : base;
+  }
+  return s.c + mv3(s.R, x_support_local(m, s, d));
 }
 
 // ------------------------------------------------------------------ MPR
@@ -414,6 +418,193 @@ __device__ __forceinline__ int mpr_penetration(const DevModel* __restrict__ m, c
       return 1;
     }
     expand_portal(p0, p1, p2, p3, v4);
+  }
+}
+
+// ------------------------------------------------------------------ MPR in fp64 (PS_MPR_F64)
+// The same algorithm with the support points and the portal arithmetic in fp64, from the fp32
+// colliders (frames, vertices, radii: a rigid rounding of each collider, which the checker's
+// state perturbation models) - the support SELECTION stays fp32 (the tie band above is ~7x its
+// rounding). Why: in fp32 the final portal, a sub-mm triangle of support points each rounded
+// independently by ~1e-9 m, has a normal with ~1e-5 rad of noise, and the termination test (the
+// portal within 1e-6 m) then flips on ~0.5% of the calls where no state perturbation does
+// (round 6).
+struct d3 {
+  double x, y, z;
+};
+__device__ __forceinline__ d3 mkd3(double a, double b, double c) { return {a, b, c}; }
+__device__ __forceinline__ d3 tod3(f3 a) { return {a.x, a.y, a.z}; }
+__device__ __forceinline__ f3 tof3(d3 a) { return mk3((float)a.x, (float)a.y, (float)a.z); }
+__device__ __forceinline__ d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ d3 operator*(d3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ double dotd(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ d3 crossd(d3 a, d3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ d3 nrmzd(d3 a) {
+  const double n = sqrt(dotd(a, a));
+  return n > 0.0 ? a * (1.0 / n) : a;
+}
+__device__ __forceinline__ bool mpr_zerod(double x) { return fabs(x) < 2.220446049250313e-16; }
+// support in fp64: the capsule analytically, a box / hull at its fp32-selected local point
+__device__ __forceinline__ d3 x_support_d(const DevModel* __restrict__ m, const XShape& s, d3 d) {
+  if (s.type == 0) {
+    const d3 p0 = tod3(s.p0), p1 = tod3(s.p1), ax = p1 - p0;
+    const double dn = sqrt(dotd(d, d));
+    double da = dotd(ax, d);
+    if (fabs(da) <= (double)SUP_TIE_CAP * sqrt(dotd(ax, ax)) * dn) da = 0.0;
+    const d3 base = da > 0.0 ? p1 : (da < 0.0 ? p0 : (p0 + p1) * 0.5);
+    return dn > 0.0 ? base + d * ((double)s.r / dn) : base;
+  }
+  const f3 l = x_support_local(m, s, tof3(d));
+  const double lx = l.x, ly = l.y, lz = l.z;
+  return mkd3(s.c.x + (s.R[0] * lx + s.R[1] * ly + s.R[2] * lz), s.c.y + (s.R[3] * lx + s.R[4] * ly + s.R[5] * lz),
+              s.c.z + (s.R[6] * lx + s.R[7] * ly + s.R[8] * lz));
+}
+// (witnesses a, b kept in fp32 too - 12 registers per portal point instead of 18 - measured
+// slower: 709K against 718K env-steps/s, the conversions on the chain)
+struct MprPtD {
+  d3 v, a, b;
+};
+__device__ __forceinline__ double xchg1d(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffll), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0xB1, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <bool PAIR>
+__device__ __forceinline__ MprPtD mpr_sup_d(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
+                                            const XShape& O, bool role, d3 d) {
+  MprPtD p;
+  if (!PAIR) {
+    p.a = x_support_d(m, A, d);
+    p.b = x_support_d(m, B, d * -1.0);
+  } else {
+    const d3 mine = x_support_d(m, O, role ? d * -1.0 : d);
+    const d3 oth = mkd3(xchg1d(mine.x), xchg1d(mine.y), xchg1d(mine.z));
+    p.a = role ? oth : mine;
+    p.b = role ? mine : oth;
+  }
+  p.v = p.a - p.b;
+  return p;
+}
+__device__ __forceinline__ d3 portal_dir_d(const MprPtD& p1, const MprPtD& p2, const MprPtD& p3) {
+  return nrmzd(crossd(p2.v - p1.v, p3.v - p1.v));
+}
+__device__ __forceinline__ bool portal_reach_tol_d(const MprPtD& p1, const MprPtD& p2, const MprPtD& p3,
+                                                   const MprPtD& v4, d3 dir) {
+  const double d4 = dotd(v4.v, dir);
+  return fmin(d4 - dotd(p1.v, dir), fmin(d4 - dotd(p2.v, dir), d4 - dotd(p3.v, dir))) <= 1e-6;  // (the checker's MPR_TOL)
+}
+__device__ __forceinline__ void expand_portal_d(const MprPtD& p0, MprPtD& p1, MprPtD& p2, MprPtD& p3, const MprPtD& v4) {
+  const d3 v4v0 = crossd(v4.v, p0.v);
+  if (dotd(p1.v, v4v0) > 0.0) {
+    if (dotd(p2.v, v4v0) > 0.0) p1 = v4; else p3 = v4;
+  } else {
+    if (dotd(p3.v, v4v0) > 0.0) p2 = v4; else p1 = v4;
+  }
+}
+__device__ __forceinline__ d3 tri_closest_origin_dd(d3 a, d3 b, d3 c) {
+  const d3 ab = b - a, ac = c - a;
+  const double d1 = -dotd(ab, a), d2 = -dotd(ac, a);
+  if (d1 <= 0.0 && d2 <= 0.0) return a;
+  const double d3_ = -dotd(ab, b), d4 = -dotd(ac, b);
+  if (d3_ >= 0.0 && d4 <= d3_) return b;
+  const double vc = d1 * d4 - d3_ * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && d3_ <= 0.0) return a + ab * (d1 / (d1 - d3_));
+  const double d5 = -dotd(ab, c), d6 = -dotd(ac, c);
+  if (d6 >= 0.0 && d5 <= d6) return c;
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) return a + ac * (d2 / (d2 - d6));
+  const double va = d3_ * d6 - d5 * d4;
+  if (va <= 0.0 && (d4 - d3_) >= 0.0 && (d5 - d6) >= 0.0) return b + (c - b) * ((d4 - d3_) / ((d4 - d3_) + (d5 - d6)));
+  const double den = 1.0 / (va + vb + vc);
+  return a + ab * (vb * den) + ac * (vc * den);
+}
+__device__ __forceinline__ d3 mpr_pos_d(const MprPtD& p0, const MprPtD& p1, const MprPtD& p2, const MprPtD& p3) {
+  const d3 dir = portal_dir_d(p1, p2, p3);
+  double b0 = dotd(crossd(p1.v, p2.v), p3.v), b1 = dotd(crossd(p3.v, p2.v), p0.v);
+  double b2 = dotd(crossd(p0.v, p1.v), p3.v), b3 = dotd(crossd(p2.v, p1.v), p0.v);
+  double sum = b0 + b1 + b2 + b3;
+  if (mpr_zerod(sum) || sum < 0.0) {
+    b0 = 0.0;
+    b1 = dotd(crossd(p2.v, p3.v), dir);
+    b2 = dotd(crossd(p3.v, p1.v), dir);
+    b3 = dotd(crossd(p1.v, p2.v), dir);
+    sum = b1 + b2 + b3;
+  }
+  const double inv = 1.0 / sum;
+  const d3 pa = p0.a * b0 + p1.a * b1 + p2.a * b2 + p3.a * b3;
+  const d3 pb = p0.b * b0 + p1.b * b1 + p2.b * b2 + p3.b * b3;
+  return (pa * inv + pb * inv) * 0.5;
+}
+// mpr_penetration in fp64 (same control flow, the checker's mpr_penetration statement for statement)
+template <bool PAIR = false>
+__device__ __forceinline__ int mpr_penetration_d(const DevModel* __restrict__ m, const XShape& A, const XShape& B,
+                                                 float* depth, f3* n, f3* pos, int* its = nullptr,
+                                                 const XShape* O = nullptr, bool role = false) {
+  const XShape& own = PAIR ? *O : A;
+  MprPtD p0, p1, p2, p3;
+  p0.a = tod3(A.c); p0.b = tod3(B.c); p0.v = p0.a - p0.b;
+  if (p0.v.x == 0.0 && p0.v.y == 0.0 && p0.v.z == 0.0) p0.v.x += 10.0 * 2.220446049250313e-16;
+  d3 dir = nrmzd(p0.v * -1.0);
+  p1 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
+  double dt = dotd(p1.v, dir);
+  if (mpr_zerod(dt) || dt < 0.0) return 0;
+  dir = crossd(p0.v, p1.v);
+  if (mpr_zerod(dotd(dir, dir))) {
+    *pos = tof3((p1.a + p1.b) * 0.5);
+    if (p1.v.x == 0.0 && p1.v.y == 0.0 && p1.v.z == 0.0) { *depth = 0.f; *n = mk3(0.f, 0.f, 0.f); }
+    else { *depth = (float)sqrt(dotd(p1.v, p1.v)); *n = tof3(nrmzd(p1.v)); }
+    return 1;
+  }
+  dir = nrmzd(dir);
+  p2 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
+  dt = dotd(p2.v, dir);
+  if (mpr_zerod(dt) || dt < 0.0) return 0;
+  dir = nrmzd(crossd(p1.v - p0.v, p2.v - p0.v));
+  if (dotd(dir, p0.v) > 0.0) { const MprPtD t = p1; p1 = p2; p2 = t; dir = dir * -1.0; }
+  for (int it = 0;; it++) {
+    if (its) ++*its;
+    if (it > 4 * MPR_MAXITF) return 0;
+    p3 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
+    dt = dotd(p3.v, dir);
+    if (mpr_zerod(dt) || dt < 0.0) return 0;
+    bool cont = false;
+    double t = dotd(crossd(p1.v, p3.v), p0.v);
+    if (t < 0.0 && !mpr_zerod(t)) { p2 = p3; cont = true; }
+    if (!cont) {
+      t = dotd(crossd(p3.v, p2.v), p0.v);
+      if (t < 0.0 && !mpr_zerod(t)) { p1 = p3; cont = true; }
+    }
+    if (!cont) break;
+    dir = nrmzd(crossd(p1.v - p0.v, p2.v - p0.v));
+  }
+  for (int it = 0;; it++) {
+    if (its) ++*its;
+    if (it > 4 * MPR_MAXITF) return 0;
+    dir = portal_dir_d(p1, p2, p3);
+    dt = dotd(p1.v, dir);
+    if (mpr_zerod(dt) || dt > 0.0) break;
+    const MprPtD v4 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
+    const double d4 = dotd(v4.v, dir);
+    if (!(mpr_zerod(d4) || d4 > 0.0) || portal_reach_tol_d(p1, p2, p3, v4, dir)) return 0;
+    expand_portal_d(p0, p1, p2, p3, v4);
+  }
+  for (int it = 0;; it++) {
+    if (its) ++*its;
+    dir = portal_dir_d(p1, p2, p3);
+    const MprPtD v4 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
+    if (portal_reach_tol_d(p1, p2, p3, v4, dir) || it > MPR_MAXITF) {
+      const d3 cp = tri_closest_origin_dd(p1.v, p2.v, p3.v);
+      const double dep = sqrt(dotd(cp, cp));
+      *depth = (float)dep;
+      *n = tof3(mpr_zerod(dep) ? dir : cp * (1.0 / dep));
+      *pos = tof3(mpr_pos_d(p0, p1, p2, p3));
+      return 1;
+    }
+    expand_portal_d(p0, p1, p2, p3, v4);
   }
 }
 
@@ -669,7 +860,11 @@ __device__ __forceinline__ int x_narrow(const DevModel* __restrict__ m, const XS
   }
   float depth;
   f3 n, p;
-  const int cnt = mpr_penetration<PAIR>(m, A, B, &depth, &n, &p, its, O, role);
+#ifndef PS_MPR_F64
+#define PS_MPR_F64 1
+#endif
+  const int cnt = PS_MPR_F64 ? mpr_penetration_d<PAIR>(m, A, B, &depth, &n, &p, its, O, role)
+                             : mpr_penetration<PAIR>(m, A, B, &depth, &n, &p, its, O, role);
   if (n.x == 0.f && n.y == 0.f && n.z == 0.f) n = mk3(0.f, 0.f, 1.f);
   pos[0] = p;
   nrm[0] = n;
