@@ -1,7 +1,8 @@
 """The step kernel's two register budgets (pianosim_kernel<XG, WPE>): launches of at most one env
-per SIMD take the one-wave instantiation (256 VGPRs + ~145 AGPRs; scratch 0 B per lane for the
-capsule kernel, ~310 B for the box/hull one), larger ones the two-wave instantiation (256 VGPRs,
-scratch ~660 / ~950 B per lane; tools/resource_usage.sh) - csrc/pianosim.hip launch(). Both
+per SIMD take the one-wave instantiation (256 VGPRs + ~143 AGPRs; scratch 0 B per lane for the
+capsule kernel, ~460 B for the box/hull one), larger ones the two-wave instantiation (256 VGPRs,
+scratch ~660 / ~1220 B per lane; round 6, fp64 MPR; tools/resource_usage.sh) - csrc/pianosim.hip
+launch(). Both
 compile the same source, so
 every output must be bitwise equal; PIANOSIM_ONE_WAVE_MAX (read by ps_create) moves the
 threshold so one small batch runs through each."""
