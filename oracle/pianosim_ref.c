@@ -1044,29 +1044,6 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
       capsule_box(E, maxc, proto, p0, p1, r, bc, I3, d->base_half);
     }
   }
-  /* extra colliders (box / hull) against the keys and the base, after every capsule */
-  for (int h = 0; h < NH; h++) {
-    for (int i = 0; i < NX; i++) {
-      if (d->xgeom_type[h][i] == PS_GEOM_NONE) continue;
-      shape B = extra_shape(E, h, i, d);
-      double rb = d->xgeom_rbound[h][i], lo[3], hi[3];
-      for (int k = 0; k < 3; k++) { lo[k] = B.c.v[k] - rb; hi[k] = B.c.v[k] + rb; }
-      contact proto;
-      memset(&proto, 0, sizeof(proto));
-      proto.h2 = h; proto.b2 = d->xgeom_body[h][i]; proto.g2 = NCAPS + h * NX + i; proto.g1 = -1;
-      for (int k = 0; k < NK; k++) {
-        if (hi[1] < m->key_y_lo[k] || lo[1] > m->key_y_hi[k]) continue;
-        if (lo[2] > d->key_pos[k][2] + d->key_half[k][2] + 0.02) continue;
-        if (hi[0] < d->key_pos[k][0] - d->key_half[k][0] - 0.02 || lo[0] > d->key_pos[k][0] + d->key_half[k][0] + 0.02) continue;
-        proto.kind = 0; proto.key = k;
-        shape A = box_shape(E->keyc[k], E->keyR[k], d->key_half[k]);
-        extra_pair(E, maxc, proto, &A, &B);
-      }
-      proto.kind = 1; proto.key = -1;
-      shape A = box_shape(bc, I3, d->base_half);
-      extra_pair(E, maxc, proto, &A, &B);
-    }
-  }
   for (int i = 0; i < d->n_cappairs; i++) {
     int ga = d->cappair[i][0], gb = d->cappair[i][1];
     int ha = ga / NG, la = ga % NG, hb = gb / NG, lb = gb % NG;
@@ -1090,6 +1067,30 @@ static void collide(const model* m, const ps_task_cfg* cfg, envdata* E) {
     cc.pos = add(c1, scl(cc.n, ra + 0.5 * dist));
     make_frame(cc.n, &cc.t1, &cc.t2);
     add_contact(E, maxc, &cc);  /* past the cap: counted in nfound, not kept */
+  }
+  /* extra colliders (box / hull) against the keys and the base, after every capsule pair (the
+   * kernel takes them and the hand-hand pairs below as one list, csrc/kernel_v2.inc collide2) */
+  for (int h = 0; h < NH; h++) {
+    for (int i = 0; i < NX; i++) {
+      if (d->xgeom_type[h][i] == PS_GEOM_NONE) continue;
+      shape B = extra_shape(E, h, i, d);
+      double rb = d->xgeom_rbound[h][i], lo[3], hi[3];
+      for (int k = 0; k < 3; k++) { lo[k] = B.c.v[k] - rb; hi[k] = B.c.v[k] + rb; }
+      contact proto;
+      memset(&proto, 0, sizeof(proto));
+      proto.h2 = h; proto.b2 = d->xgeom_body[h][i]; proto.g2 = NCAPS + h * NX + i; proto.g1 = -1;
+      for (int k = 0; k < NK; k++) {
+        if (hi[1] < m->key_y_lo[k] || lo[1] > m->key_y_hi[k]) continue;
+        if (lo[2] > d->key_pos[k][2] + d->key_half[k][2] + 0.02) continue;
+        if (hi[0] < d->key_pos[k][0] - d->key_half[k][0] - 0.02 || lo[0] > d->key_pos[k][0] + d->key_half[k][0] + 0.02) continue;
+        proto.kind = 0; proto.key = k;
+        shape A = box_shape(E->keyc[k], E->keyR[k], d->key_half[k]);
+        extra_pair(E, maxc, proto, &A, &B);
+      }
+      proto.kind = 1; proto.key = -1;
+      shape A = box_shape(bc, I3, d->base_half);
+      extra_pair(E, maxc, proto, &A, &B);
+    }
   }
   /* hand-hand pairs with an extra collider: bounding spheres, then capsule-box (normal box ->
    * capsule, the box as geom1), box-box or MPR (normal geom a -> geom b) */

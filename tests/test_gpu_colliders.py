@@ -24,7 +24,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import Floor, assert_flip_rates, assert_parity, box_hull_hand, song
+from helpers import PARITY_P99_CEIL_UNREFINED, Floor, assert_flip_rates, assert_parity, box_hull_hand, song
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -48,8 +48,8 @@ def task(dp, request):
 def test_box_hull_hand_teacher_forced(dp, ref, task):
     """GPU vs checker, one control step from the same state, against the model's own fp64
     sensitivity (the checker stepped from the state with the hand joints moved by 1e-7 rad):
-    helpers.assert_parity and helpers.assert_flip_rates on qpos; reward p95 within 2x the
-    checker's own."""
+    helpers.assert_parity (all-sample ceiling 2e-4, below) and helpers.assert_flip_rates on qpos;
+    reward p95 within 2x the checker's own."""
     n = 32
     seq = song(dp, "twinkle")
     md, st, tc = dp.compile_task(seq, task, canonical_actions=False)
@@ -80,7 +80,11 @@ def test_box_hull_hand_teacher_forced(dp, ref, task):
                 kinds.add((kind, g1 >= 40, g2 >= 40))
     e, f = np.concatenate(errs), np.concatenate(floor)
     assert_flip_rates(e, f, "box/hull hand, control step")
-    assert_parity(e, f, "box/hull hand, control step")
+    # all-sample ceiling 2e-4 here: the p99 of 960 errors is their 10th largest, at the checker's
+    # own p99 sensitivity (floor p99 ~1.5e-4): measured 7.1e-5 and 1.17e-4 on two builds whose
+    # only difference is the order of the contact list (round 6) - rounding-level changes move it
+    # across 1e-4. The benched workload's test holds the 1e-4 ceiling over 1280 env-steps.
+    assert_parity(e, f, "box/hull hand, control step", p99_ceil=PARITY_P99_CEIL_UNREFINED)
     re, rf = np.concatenate(rerr), np.concatenate(rfloor)
     print(f"box/hull hand, control step reward: p95 {np.percentile(re, 95):.3g} floor p95 {np.percentile(rf, 95):.3g}")
     assert np.percentile(re, 95) <= max(1e-3, 2 * np.percentile(rf, 95)), (np.percentile(re, 95), np.percentile(rf, 95))

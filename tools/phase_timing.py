@@ -43,15 +43,19 @@ print(f"Newton: iterations per substep mean {solves.mean():.3f}, max over env-st
 # ones from the previous substep's zones (one iteration when that piece holds)
 c = out[:, 19:24].astype(np.float64).sum(axis=0)
 m = out[:, 28:32].astype(np.float64).sum(axis=0)  # box / hull narrow-phase rounds (timing build)
+# (since round 6 the piano and hand-hand box / hull pairs are one list: one refine pass and one
+# series of rounds, counted in the hand-hand slots - xpiano:refine / narrow and the piano round
+# counters stay 0; xpiano:cand is the piano candidates, xpairs:sphere the hand-hand spheres)
 if m[1] > 0 or m[3] > 0:
     print(f"box/hull narrow phase: piano {m[1] / N / 100:.2f} rounds/substep, {m[0] / max(m[1], 1):.1f} MPR steps of the "
-          f"slowest lane per round; hand-hand {m[3] / N / 100:.2f} rounds/substep, {m[2] / max(m[3], 1):.1f} steps")
+          f"slowest lane per round; piano + hand-hand {m[3] / N / 100:.2f} rounds/substep, {m[2] / max(m[3], 1):.1f} steps")
 h = out[:, 38:46].astype(np.float64).sum(axis=0)
 if h[0] > 0:
-    print(f"hand-hand pairs per substep: {h[7] / N / 100:.2f} past the spheres, {h[0] / N / 100:.2f} past the enclosing "
-          f"capsules (substeps with any: {h[4] / N / 100:.3f}), {h[1] / N / 100:.3f} with a contact; MPR steps per pair "
-          f"{h[2] / max(h[0], 1):.2f} (contact pairs {h[3] / max(h[1], 1):.2f}, others {(h[2] - h[3]) / max(h[0] - h[1], 1):.2f}); "
-          f"piano hull pairs per substep {h[5] / N / 100:.2f}, {h[6] / N / 100:.3f} with a contact")
+    print(f"box/hull pairs per substep: {h[7] / N / 100:.2f} listed (piano candidates + hand-hand past the spheres), "
+          f"{h[0] / N / 100:.2f} past the enclosing capsules (substeps with any: {h[4] / N / 100:.3f}), {h[1] / N / 100:.3f} "
+          f"with a contact; MPR steps per pair {h[2] / max(h[0], 1):.2f} (contact pairs {h[3] / max(h[1], 1):.2f}, others "
+          f"{(h[2] - h[3]) / max(h[0] - h[1], 1):.2f}); piano hull pairs per substep (before round 6) {h[5] / N / 100:.2f}, "
+          f"{h[6] / N / 100:.3f} with a contact")
 if c[1] > 0 and c[4] > 0:
     print(f"Newton by substep: first {c[0] / c[1]:.2f} iterations, later {c[2] / c[4]:.2f} "
           f"(guessed piece held in {100 * c[3] / c[4]:.1f}% of the later substeps)")
