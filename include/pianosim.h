@@ -338,8 +338,10 @@ typedef struct {
 } ps_contact;
 /* Contact lists of each env's last step: ps_record_contacts(env, 1) makes the step kernel
  * keep them (off by default: ~70 B per contact of extra HBM writes); ps_contacts copies them
- * to out [N][PS_MAX_CONTACTS_LIMIT] (device; the first ncon of each env are valid). No
- * reference counterpart beyond physics.data.contact; used for collision parity checks. */
+ * to out [N][PS_MAX_CONTACTS_LIMIT] (device; the first ncon of each env are valid), in the
+ * order capsule-piano, capsule-capsule, box / hull-piano, box / hull hand-hand (round 6; the
+ * checker's, oracle/pianosim_ref.c collide). No reference counterpart beyond
+ * physics.data.contact; used for collision parity checks. */
 int ps_record_contacts(ps_env* env, int on);
 int ps_contacts(ps_env* env, ps_contact* out, void* stream);
 
