@@ -227,7 +227,18 @@ def test_mjcf_box_and_mesh_colliders(dp, tmp_path):
         mj.load_hand(big)
 
 
+def _contact_phase(kind, g1, g2):
+    """the collision phase of a contact in the checker's (and the kernel's) list order: 0
+    capsule-piano, 1 capsule-capsule, 2 box / hull-piano, 3 box / hull hand-hand"""
+    if kind in (0, 1):
+        return 2 if g2 >= 40 else 0
+    return 3 if g1 >= 40 or g2 >= 40 else 1
+
+
 def test_oracle_rollout_with_box_and_hull_colliders(dp, ref):
+    """The box / hull hand steps finite in the checker, with key-hull, hull-capsule and
+    hull-hull contacts, each env's contact list in the phase order the kernel writes (round 6:
+    csrc/kernel_v2.inc collide2 takes the box / hull pairs after every capsule pair, as one list)."""
     hand = box_hull_hand(dp)
     task = dp.TaskConfig(hand_xml=dp.mjcf.hand_to_mjcf(hand))
     md, st, tc = dp.compile_task(song(dp, "twinkle"), task, canonical_actions=False)
@@ -236,17 +247,22 @@ def test_oracle_rollout_with_box_and_hull_colliders(dp, ref):
     o.reset()
     lo, hi = dp.model.action_spec(md)
     rng = np.random.RandomState(0)
-    kinds = set()
+    kinds, phases = set(), set()
     for _ in range(60):
         o.step(rng.uniform(lo, hi, (n, 45)).astype(np.float32))
         for i in range(n):
-            for kind, key, g1, g2, dist in o.contacts(i):
+            cs = o.contacts(i)
+            order = [_contact_phase(kind, g1, g2) for kind, key, g1, g2, dist in cs]
+            assert order == sorted(order), cs
+            phases.update(order)
+            for kind, key, g1, g2, dist in cs:
                 assert dist <= 1e-12
                 t1 = "key" if kind == 0 else ("base" if kind == 1 else ("x" if g1 >= 40 else "c"))
                 kinds.add((t1, "x" if g2 >= 40 else "c"))
     s = o.get_state()
     assert np.isfinite(s["qpos"]).all() and np.isfinite(s["qvel"]).all()
     assert {("key", "x"), ("x", "c"), ("x", "x")} <= kinds, kinds
+    assert {0, 2, 3} <= phases, phases
 
 
 def test_mpr_support_ties_are_stable(ref, dp):

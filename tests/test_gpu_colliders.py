@@ -369,8 +369,11 @@ def test_benched_workload_contact_lists(dp, ref):
     cg = g.contacts()
     o = ref.OracleEnv(md, st, tc, N)
     o.set_state(s)
-    total, bad = 0, Counter()
+    total, bad, unordered = 0, Counter(), 0
     for i in range(N):
+        # the GPU's list in the checker's phase order (test_colliders._contact_phase)
+        ph = [(2 if x[3] >= 40 else 0) if x[0] in (0, 1) else (3 if x[2] >= 40 or x[3] >= 40 else 1) for x in cg[i]]
+        unordered += ph != sorted(ph)
         co = o.contacts_full(i)
         used = set()
         for c in co:
@@ -391,6 +394,7 @@ def test_benched_workload_contact_lists(dp, ref):
     nbad = sum(bad.values())
     print(f"bench workload contact lists: {total} contacts, {nbad} mismatches {dict(bad)}")
     assert total > 10000
+    assert unordered == 0
     assert nbad <= 0.003 * total, dict(bad)
     # (hull-key pairs run the same MPR: its termination test could flip there too, rarely)
     assert sum(v for (_, kind), v in bad.items() if kind != "hand-hand") <= 3, dict(bad)
