@@ -517,13 +517,25 @@ __device__ __forceinline__ bool portal_reach_tol_d(const MprPtD& p1, const MprPt
   const double d4 = dotd(v4.v, dir);
   return fmin(d4 - dotd(p1.v, dir), fmin(d4 - dotd(p2.v, dir), d4 - dotd(p3.v, dir))) <= 1e-6;  // (the checker's MPR_TOL)
 }
+// c ? a : b field by field (values: a conditional assignment of whole portal points became a
+// store through a selected address, the portal in scratch memory)
+__device__ __forceinline__ d3 seld(bool c, d3 a, d3 b) { return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
+__device__ __forceinline__ MprPtD selp(bool c, const MprPtD& a, const MprPtD& b) {
+  MprPtD r;
+  r.v = seld(c, a.v, b.v);
+  r.a = seld(c, a.a, b.a);
+  r.b = seld(c, a.b, b.b);
+  return r;
+}
 __device__ __forceinline__ void expand_portal_d(const MprPtD& p0, MprPtD& p1, MprPtD& p2, MprPtD& p3, const MprPtD& v4) {
+  // (libccd's branches: p1 . v4v0 > 0 ? (p2 . v4v0 > 0 ? p1 : p3) : (p3 . v4v0 > 0 ? p2 : p1)
+  // takes v4; all three dots formed, the point replaced by selects)
   const d3 v4v0 = crossd(v4.v, p0.v);
-  if (dotd(p1.v, v4v0) > 0.0) {
-    if (dotd(p2.v, v4v0) > 0.0) p1 = v4; else p3 = v4;
-  } else {
-    if (dotd(p3.v, v4v0) > 0.0) p2 = v4; else p1 = v4;
-  }
+  const bool s1 = dotd(p1.v, v4v0) > 0.0, s2 = dotd(p2.v, v4v0) > 0.0, s3 = dotd(p3.v, v4v0) > 0.0;
+  const bool to1 = s1 ? s2 : !s3, to2 = !s1 && s3, to3 = s1 && !s2;
+  p1 = selp(to1, v4, p1);
+  p2 = selp(to2, v4, p2);
+  p3 = selp(to3, v4, p3);
 }
 __device__ __forceinline__ d3 tri_closest_origin_dd(d3 a, d3 b, d3 c) {
   const d3 ab = b - a, ac = c - a;
@@ -584,21 +596,26 @@ __device__ __forceinline__ int mpr_penetration_d(const DevModel* __restrict__ m,
   dt = dotd(p2.v, dir);
   if (mpr_zerod(dt) || dt < 0.0) return 0;
   dir = nrmzd(crossd(p1.v - p0.v, p2.v - p0.v));
-  if (dotd(dir, p0.v) > 0.0) { const MprPtD t = p1; p1 = p2; p2 = t; dir = dir * -1.0; }
+  {
+    const bool sw = dotd(dir, p0.v) > 0.0;
+    const MprPtD t = p1;
+    p1 = selp(sw, p2, p1);
+    p2 = selp(sw, t, p2);
+    dir = sw ? dir * -1.0 : dir;
+  }
   for (int it = 0;; it++) {
     if (its) ++*its;
     if (it > 4 * MPR_MAXITF) return 0;
     p3 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
     dt = dotd(p3.v, dir);
     if (mpr_zerod(dt) || dt < 0.0) return 0;
-    bool cont = false;
-    double t = dotd(crossd(p1.v, p3.v), p0.v);
-    if (t < 0.0 && !mpr_zerod(t)) { p2 = p3; cont = true; }
-    if (!cont) {
-      t = dotd(crossd(p3.v, p2.v), p0.v);
-      if (t < 0.0 && !mpr_zerod(t)) { p1 = p3; cont = true; }
-    }
-    if (!cont) break;
+    const double t1 = dotd(crossd(p1.v, p3.v), p0.v);
+    const bool c2 = t1 < 0.0 && !mpr_zerod(t1);
+    const double t2 = dotd(crossd(p3.v, p2.v), p0.v);
+    const bool c1 = !c2 && t2 < 0.0 && !mpr_zerod(t2);
+    p2 = selp(c2, p3, p2);
+    p1 = selp(c1, p3, p1);
+    if (!c2 && !c1) break;
     dir = nrmzd(crossd(p1.v - p0.v, p2.v - p0.v));
   }
   for (int it = 0;; it++) {
@@ -838,20 +855,29 @@ __device__ __forceinline__ int capsule_obox(const XShape& C, const XShape& Bx, f
 // capsule, capsule or box) by more than 1e-5 m: the hulls are apart, MPR would find nothing.
 __device__ __forceinline__ bool x_apart(const XShape& A, const XShape& B) {
   if (A.type != PS_GEOM_HULL && B.type != PS_GEOM_HULL) return false;
+  // (every field selected by value, component by component: a reference to "the other"
+  // collider would take both colliders' addresses and put them in scratch memory)
   const bool ha = A.type == PS_GEOM_HULL;
-  const f3 h0 = ha ? A.e0 : B.e0, h1 = ha ? A.e1 : B.e1;
+  auto sel = [ha](f3 a, f3 b) { return mk3(ha ? a.x : b.x, ha ? a.y : b.y, ha ? a.z : b.z); };
+  const f3 h0 = sel(A.e0, B.e0), h1 = sel(A.e1, B.e1);
   const float hr = ha ? A.er : B.er;
-  const XShape& O = ha ? B : A;
+  const int otype = ha ? B.type : A.type;
   float d;
-  if (O.type == PS_GEOM_BOX) {
-    const float hs[3] = {O.hs.x, O.hs.y, O.hs.z};
-    const f3 a = mtv3(O.R, h0 - O.c), b = mtv3(O.R, h1 - O.c);
+  if (otype == PS_GEOM_BOX) {
+    const f3 oc = sel(B.c, A.c), ohs = sel(B.hs, A.hs);
+    float oR[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) oR[i] = ha ? B.R[i] : A.R[i];
+    const float hs[3] = {ohs.x, ohs.y, ohs.z};
+    const f3 a = mtv3(oR, h0 - oc), b = mtv3(oR, h1 - oc);
     const float t = seg_box_t(a, b - a, hs);
     f3 n, p;
-    d = sphere_box(h0 + (h1 - h0) * t, hr, O.c, O.R, hs, &n, &p);
+    d = sphere_box(h0 + (h1 - h0) * t, hr, oc, oR, hs, &n, &p);
   } else {
-    const f3 o0 = O.type == PS_GEOM_HULL ? O.e0 : O.p0, o1 = O.type == PS_GEOM_HULL ? O.e1 : O.p1;
-    const float orad = O.type == PS_GEOM_HULL ? O.er : O.r;
+    const bool oh = otype == PS_GEOM_HULL;
+    const f3 e0 = sel(B.e0, A.e0), e1 = sel(B.e1, A.e1), p0 = sel(B.p0, A.p0), p1 = sel(B.p1, A.p1);
+    const f3 o0 = oh ? e0 : p0, o1 = oh ? e1 : p1;
+    const float orad = oh ? (ha ? B.er : A.er) : (ha ? B.r : A.r);
     f3 c1, c2;
     seg_seg(h0, h1, o0, o1, &c1, &c2);
     d = norm3(c2 - c1) - hr - orad;
