@@ -517,25 +517,13 @@ __device__ __forceinline__ bool portal_reach_tol_d(const MprPtD& p1, const MprPt
   const double d4 = dotd(v4.v, dir);
   return fmin(d4 - dotd(p1.v, dir), fmin(d4 - dotd(p2.v, dir), d4 - dotd(p3.v, dir))) <= 1e-6;  // (the checker's MPR_TOL)
 }
-// c ? a : b field by field (values: a conditional assignment of whole portal points became a
-// store through a selected address, the portal in scratch memory)
-__device__ __forceinline__ d3 seld(bool c, d3 a, d3 b) { return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
-__device__ __forceinline__ MprPtD selp(bool c, const MprPtD& a, const MprPtD& b) {
-  MprPtD r;
-  r.v = seld(c, a.v, b.v);
-  r.a = seld(c, a.a, b.a);
-  r.b = seld(c, a.b, b.b);
-  return r;
-}
 __device__ __forceinline__ void expand_portal_d(const MprPtD& p0, MprPtD& p1, MprPtD& p2, MprPtD& p3, const MprPtD& v4) {
-  // (libccd's branches: p1 . v4v0 > 0 ? (p2 . v4v0 > 0 ? p1 : p3) : (p3 . v4v0 > 0 ? p2 : p1)
-  // takes v4; all three dots formed, the point replaced by selects)
   const d3 v4v0 = crossd(v4.v, p0.v);
-  const bool s1 = dotd(p1.v, v4v0) > 0.0, s2 = dotd(p2.v, v4v0) > 0.0, s3 = dotd(p3.v, v4v0) > 0.0;
-  const bool to1 = s1 ? s2 : !s3, to2 = !s1 && s3, to3 = s1 && !s2;
-  p1 = selp(to1, v4, p1);
-  p2 = selp(to2, v4, p2);
-  p3 = selp(to3, v4, p3);
+  if (dotd(p1.v, v4v0) > 0.0) {
+    if (dotd(p2.v, v4v0) > 0.0) p1 = v4; else p3 = v4;
+  } else {
+    if (dotd(p3.v, v4v0) > 0.0) p2 = v4; else p1 = v4;
+  }
 }
 __device__ __forceinline__ d3 tri_closest_origin_dd(d3 a, d3 b, d3 c) {
   const d3 ab = b - a, ac = c - a;
@@ -596,26 +584,21 @@ __device__ __forceinline__ int mpr_penetration_d(const DevModel* __restrict__ m,
   dt = dotd(p2.v, dir);
   if (mpr_zerod(dt) || dt < 0.0) return 0;
   dir = nrmzd(crossd(p1.v - p0.v, p2.v - p0.v));
-  {
-    const bool sw = dotd(dir, p0.v) > 0.0;
-    const MprPtD t = p1;
-    p1 = selp(sw, p2, p1);
-    p2 = selp(sw, t, p2);
-    dir = sw ? dir * -1.0 : dir;
-  }
+  if (dotd(dir, p0.v) > 0.0) { const MprPtD t = p1; p1 = p2; p2 = t; dir = dir * -1.0; }
   for (int it = 0;; it++) {
     if (its) ++*its;
     if (it > 4 * MPR_MAXITF) return 0;
     p3 = mpr_sup_d<PAIR>(m, A, B, own, role, dir);
     dt = dotd(p3.v, dir);
     if (mpr_zerod(dt) || dt < 0.0) return 0;
-    const double t1 = dotd(crossd(p1.v, p3.v), p0.v);
-    const bool c2 = t1 < 0.0 && !mpr_zerod(t1);
-    const double t2 = dotd(crossd(p3.v, p2.v), p0.v);
-    const bool c1 = !c2 && t2 < 0.0 && !mpr_zerod(t2);
-    p2 = selp(c2, p3, p2);
-    p1 = selp(c1, p3, p1);
-    if (!c2 && !c1) break;
+    bool cont = false;
+    double t = dotd(crossd(p1.v, p3.v), p0.v);
+    if (t < 0.0 && !mpr_zerod(t)) { p2 = p3; cont = true; }
+    if (!cont) {
+      t = dotd(crossd(p3.v, p2.v), p0.v);
+      if (t < 0.0 && !mpr_zerod(t)) { p1 = p3; cont = true; }
+    }
+    if (!cont) break;
     dir = nrmzd(crossd(p1.v - p0.v, p2.v - p0.v));
   }
   for (int it = 0;; it++) {
