@@ -285,8 +285,11 @@ __device__ __forceinline__ float seg_box_t(f3 a3, f3 d3, const float* hs) {
 // The box frame is a rotation about +y (keys; the base: cq = 1, sq = 0) and comes in by
 // value, like the half sizes: arrays passed by pointer to an out-of-line function live in
 // scratch memory, a store/load round trip through the vector memory path per call.
+#ifndef PS_CBOX_ATTR
+#define PS_CBOX_ATTR __noinline__
+#endif
 template <int WPE>  // the calling kernel's waves per SIMD (one out-of-line copy per register budget)
-__device__ __noinline__ int capsule_box(f3 p0, f3 p1, float r, f3 c, float cq, float sq, f3 hsv, Contact* out, int slot,
+__device__ PS_CBOX_ATTR int capsule_box(f3 p0, f3 p1, float r, f3 c, float cq, float sq, f3 hsv, Contact* out, int slot,
                            int maxc, int kind, int key, int g2) {
   const float R[9] = {cq, 0.f, sq, 0.f, 1.f, 0.f, -sq, 0.f, cq};
   const float hs[3] = {hsv.x, hsv.y, hsv.z};
